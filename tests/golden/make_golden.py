@@ -1,0 +1,71 @@
+"""Generate the golden fixtures in tests/golden/ by running the REFERENCE's own
+code (oracle/_ref/ref_harness, built by `make -C oracle ref` from
+/root/reference -- development container only).  The fixtures are data: scene
+descriptions (inputs) and the reference's outputs for them.
+
+    python tests/golden/make_golden.py
+
+Fixture list and layouts: tests/golden/README.md.
+"""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "simple-raytracing-render_amd"))
+
+from srr import scenes  # noqa: E402
+
+HARNESS = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+
+# (name, scene factory, nx, ny, spp, max_depth)
+RENDERS = [
+    ("s1", lambda: scenes.s1_cornell()[0], 32, 32, 16, 50),
+    ("s2", lambda: scenes.s2_cornell_teapot()[0], 32, 32, 16, 50),
+    ("s3", lambda: scenes.s3_cornell_teapot_microfacet()[0], 32, 32, 16, 50),
+    ("s3_metal", lambda: scenes.s3_cornell_teapot_microfacet("metal")[0], 32, 32, 16, 50),
+    ("s4_small", lambda: scenes.s4_soldier_standin(divs=8)[0], 32, 18, 8, 50),
+    ("s5_small", lambda: scenes.s4_soldier_standin(divs=8, fog=True)[0], 32, 18, 8, 50),
+    ("s2_depth3", lambda: scenes.s2_cornell_teapot()[0], 16, 16, 8, 3),
+]
+
+KATS = [("erf", 512), ("beckmann11", 512), ("beckmann_dist", 512), ("beckmann_pdf", 512), ("cosine_pdf", 256),
+        ("orennayar_pdf", 256), ("dielectric", 256), ("metal", 256), ("triangle", 1024), ("aabb", 1024),
+        ("camera", 256), ("lights", 256)]
+
+
+def run(*args):
+    out = subprocess.run([HARNESS, *map(str, args)], check=True, capture_output=True, text=True)
+    return out.stdout
+
+
+def main():
+    if not os.path.exists(HARNESS):
+        sys.exit("build the reference harness first: make -C oracle ref")
+    meta = {"renders": {}, "kats": {}}
+    for name, fac, nx, ny, spp, md in RENDERS:
+        txt = os.path.join(HERE, f"{name}.scene")
+        with open(txt, "w") as f:
+            f.write(fac().text())
+        stats = json.loads(run("render", txt, nx, ny, spp, md, os.path.join(HERE, name)).strip().splitlines()[-1])
+        os.remove(os.path.join(HERE, f"{name}.ppm"))
+        meta["renders"][name] = dict(nx=nx, ny=ny, spp=spp, max_depth=md, world_rays=stats["world_rays"])
+        print(name, stats)
+    for name, n in KATS:
+        run("kat", name, n, 1234567, os.path.join(HERE, f"kat_{name}.bin"))
+        meta["kats"][name] = n
+    run("teapot", 60.0, 10, os.path.join(HERE, "teapot_s60_d10.f32"))
+    for n in (64, 1024, 4096):
+        run("sobol", n, os.path.join(HERE, f"sobol_{n}.f64"))
+    # reference BVH topology of S2's teapot (object 11 = bvh_group)
+    run("bvh", os.path.join(HERE, "s2.scene"), 11, os.path.join(HERE, "bvh_s2_teapot.txt"))
+    with open(os.path.join(HERE, "golden.json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()
