@@ -1,0 +1,180 @@
+/* srr -- MI355X-native path tracer: C-ABI drop-in boundary.
+ *
+ * The reference (truemeat001/Simple-Raytracing-Render) has no FFI: its
+ * "operator API" is a C++ class hierarchy that scene builders instantiate with
+ * `new` (Raytracing_n.cpp:108-711) and a render driver walks on 8 CPU threads
+ * (renderthread, Raytracing_n.cpp:815-879).  This header is that boundary as a
+ * flat C ABI: one constructor per reference class (same argument order and
+ * meaning), returning integer handles, plus the render entry points that
+ * replace renderthread/main.  Plain pointers and sizes only; no C++ or torch
+ * types.  Every function returns >= 0 on success and a negative errno-style code
+ * on failure (srr_last_error() has the message); nothing calls exit()
+ * (the reference's sobol_points does, Raytracing_n.cpp:724-727).
+ *
+ * Threading: a scene / renderer handle is used by one host thread at a time.
+ * The C++ source-compatible headers in include/srr/ are a thin layer over this
+ * ABI (see INTEGRATION.md for the ctypes / C++ bindings).
+ */
+#ifndef SRR_CAPI_H
+#define SRR_CAPI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SRR_OK 0
+#define SRR_EINVAL (-22)
+#define SRR_ENOMEM (-12)
+#define SRR_ENODEV (-19)
+#define SRR_ENOTSUP (-95)
+#define SRR_EIO (-5)
+
+typedef struct srr_scene srr_scene;
+typedef struct srr_renderer srr_renderer;
+
+/* Thread-local message for the last failing call on this thread. */
+const char* srr_last_error(void);
+/* Library version / build string ("srr 0.1 gfx950 ..."). */
+const char* srr_version(void);
+
+/* ------------------------------------------------------------ scene lifetime */
+srr_scene* srr_scene_create(void);
+void srr_scene_destroy(srr_scene* s);
+/* Parse an srr scene description v1 into a new scene. */
+int srr_scene_from_text(const char* text, srr_scene** out);
+/* Handle of the hitable a parsed description named `obj <text_id>`. */
+int srr_scene_text_handle(const srr_scene* s, int text_id);
+/* State of the scene-build LCG (the reference's global drand48 seed,
+ * mathf.h:12) that the next srr_bvh_node() consumes; default is the
+ * post-Perlin state 24561125610955 (perlin.h:94-97). */
+int srr_scene_set_lcg(srr_scene* s, uint64_t state);
+uint64_t srr_scene_get_lcg(const srr_scene* s);
+/* drand48() on the scene LCG (mathf.h:14-19), for builders that draw. */
+double srr_scene_drand48(srr_scene* s);
+
+/* ------------------------------------------------------------------ textures
+ * texture.h:25-33 constant_texture(vec3) */
+int srr_constant_texture(srr_scene* s, float r, float g, float b);
+/* texture.h:48-70 image_texture(unsigned char* pixels, int nx, int ny): RGB8,
+ * row 0 = top; the bytes are copied (the reference borrows them). */
+int srr_image_texture(srr_scene* s, const unsigned char* rgb, int nx, int ny);
+/* Synthetic RGB8 image (stand-in for stbi_load'ed assets; kind 0 sky, 1 wood,
+ * 2 checker), identical bytes on every consumer. */
+int srr_image_texture_gen(srr_scene* s, int nx, int ny, uint32_t seed, int kind);
+/* texture.h:9-23 checker_texture(texture* t0 (even), texture* t1 (odd)) */
+int srr_checker_texture(srr_scene* s, int even_tex, int odd_tex);
+/* texture.h:35-46 noise_texture(float scale) (Perlin tables of perlin.h:67-97) */
+int srr_noise_texture(srr_scene* s, float scale);
+
+/* ----------------------------------------------------------------- materials
+ * (material.h); a material handle of -1 is the reference's null material* */
+int srr_lambertian(srr_scene* s, int albedo_tex);                       /* :95-114  */
+int srr_orennayar(srr_scene* s, int albedo_tex, float sigma_deg);       /* :127-149 */
+int srr_beckmann(srr_scene* s, int albedo_tex, float roughx, float roughy); /* :151-199 */
+int srr_metal(srr_scene* s, float r, float g, float b, float fuzz);     /* :243-261 */
+int srr_dielectric(srr_scene* s, float ref_idx);                        /* :282-339 */
+int srr_diffuse_light(srr_scene* s, int emit_tex);                      /* :341-356 */
+int srr_isotropic(srr_scene* s, int albedo_tex);                        /* :359-369 */
+
+/* ------------------------------------------------------------------ hitables */
+int srr_sphere(srr_scene* s, const float center[3], float radius, int mat);        /* sphere.h:21 */
+int srr_moving_sphere(srr_scene* s, const float c0[3], const float c1[3], float t0, float t1, float radius,
+                      int mat);                                                     /* moving_sphere.h:8 */
+int srr_xy_rect(srr_scene* s, float x0, float x1, float y0, float y1, float k, int mat); /* aarect.h:8 */
+int srr_xz_rect(srr_scene* s, float x0, float x1, float z0, float z1, float k, int mat); /* aarect.h:38 */
+int srr_yz_rect(srr_scene* s, float y0, float y1, float z0, float z1, float k, int mat); /* aarect.h:69 */
+int srr_box(srr_scene* s, const float p0[3], const float p1[3], int mat);          /* box.h:18-29 */
+/* triangle.h:13-50: uv (3 x vec3) and normals (3 x vec3) may be NULL; without
+ * normals the face normal is used (SURVEY Q5 build definition). */
+int srr_triangle(srr_scene* s, const float p[9], int mat, const float* uv9, const float* n9);
+int srr_flip_normals(srr_scene* s, int child);                                     /* aarect.h:149-171 */
+int srr_translate(srr_scene* s, int child, const float offset[3]);                 /* hitable.h:35-61 */
+int srr_rotate_y(srr_scene* s, int child, float angle_deg);                        /* hitable.h:65-132 */
+int srr_rotate_x(srr_scene* s, int child, float angle_deg);                        /* hitable.h:135-203 */
+int srr_constant_medium(srr_scene* s, int boundary, float density, int tex);       /* constant_medium.h:6 */
+int srr_hitable_list(srr_scene* s, const int* children, int n);                    /* hitable_list.h:11 */
+/* bvh.h:96-119 bvh_node(hitable** l, int n, float time0, float time1): built
+ * eagerly with the reference's random-axis median split, consuming the scene
+ * LCG exactly like the reference (one draw per node). */
+int srr_bvh_node(srr_scene* s, const int* children, int n, float time0, float time1);
+/* Utah teapot (teapot.h:76-166) with `divs` subdivisions: creates 2*32*divs^2
+ * triangle handles, first_handle .. first_handle+count-1, returns count. */
+int srr_teapot(srr_scene* s, float scale, int divs, int mat, int* first_handle);
+/* Handles of [first, first+count) as an array for list/bvh constructors. */
+
+/* camera.h:33-48, 9-argument constructor */
+int srr_camera(srr_scene* s, const float lookfrom[3], const float lookat[3], const float vup[3], float vfov,
+               float aspect, float aperture, float focus_dist, float t0, float t1);
+/* world: the hitable passed as `world` to renderthread (Raytracing_n.cpp:815);
+ * lights: `hlist`, must be a hitable_list (cast at Raytracing_n.cpp:75). */
+int srr_scene_set_world(srr_scene* s, int obj);
+int srr_scene_set_lights(srr_scene* s, int list_obj);
+
+/* ----------------------------------------------------------------- rendering */
+typedef struct srr_params {
+  int nx, ny;          /* image size (Raytracing_n.cpp:39-40)                  */
+  int spp;             /* samples per pixel, ns (:41)                          */
+  int max_depth;       /* maxDepth (:42)                                       */
+  int tile;            /* tile edge for sharding, e.g. 32                      */
+  int shard_index;     /* this renderer renders tiles t with t % shard_count   */
+  int shard_count;     /*   == shard_index                       */
+  int batch_paths;     /* paths in flight per wavefront batch (0 = auto)       */
+  uint64_t base_seed;  /* per-path seed salt; 0 = SURVEY §8(d) definition      */
+  int flags;           /* SRR_FLAG_*                                           */
+} srr_params;
+
+#define SRR_FLAG_SORT_MATERIALS 1 /* material-sorted shading (perf only)      */
+#define SRR_FLAG_KEEP_PATHS 2     /* keep per-path radiance for parity tests   */
+
+typedef struct srr_stats {
+  int64_t world_rays;   /* world->hit calls (the metric's samples)             */
+  int64_t paths;        /* camera paths                                        */
+  int64_t trace_launches;
+  double trace_ms;      /* summed HIP-event time of the trace kernel launches  */
+  double shade_ms;
+  double total_ms;      /* render wall time on the device stream               */
+  int64_t bounces;      /* bounce iterations launched                          */
+} srr_stats;
+
+/* Flatten the scene and upload it to HIP device `device`. */
+int srr_renderer_create(const srr_scene* s, int device, srr_renderer** out);
+void srr_renderer_destroy(srr_renderer* r);
+/* Number of pixels this shard renders, and their PPM-order indices (row 0 =
+ * top, Raytracing_n.cpp:873-876) into pixel_index[] (may be NULL). */
+int64_t srr_shard_pixels(const srr_params* p, int32_t* pixel_index);
+/* Render this shard.  d_mean: DEVICE pointer, n_shard_pixels*3 floats -- the
+ * per-pixel mean of de_nan'd samples before the sqrt (Raytracing_n.cpp:841-848),
+ * in srr_shard_pixels() order.  Inputs are resident on the device; the call
+ * returns after the device work finished. */
+int srr_render_device(srr_renderer* r, const srr_params* p, float* d_mean, srr_stats* stats);
+/* Host convenience: whole image (shard 0 of 1), mean (nx*ny*3, may be NULL)
+ * and 8-bit tone-mapped rgb8 (nx*ny*3, Raytracing_n.cpp:850-867, may be NULL). */
+int srr_render(srr_renderer* r, const srr_params* p, float* mean, unsigned char* rgb8, srr_stats* stats);
+/* After a render with SRR_FLAG_KEEP_PATHS: per-path raw radiance (before
+ * de_nan) and world-ray counts, [n_shard_pixels][spp]. */
+int srr_copy_paths(srr_renderer* r, float* radiance, unsigned char* rays);
+/* Tone map (Raytracing_n.cpp:850-867): 8-bit = clamp(int(255.99*sqrt(m))). */
+int srr_tonemap(const float* mean, int64_t n_pixels, unsigned char* rgb8);
+/* Write an ASCII P3 PPM (Raytracing_n.cpp:886, 873-876). */
+int srr_write_ppm(const char* path, int nx, int ny, const unsigned char* rgb8);
+
+/* Sobol (0,2)-points of Raytracing_n.cpp:721-812, out[n][2]. */
+int srr_sobol_points(int n, double* out);
+
+/* Host-side inspection (no GPU needed) -------------------------------------
+ * Teapot triangles (p0 p1 p2, 9 floats each) as srr_teapot would create them;
+ * returns the triangle count (out may be NULL to query it). */
+int srr_teapot_vertices(float scale, int divs, float* out);
+/* Topology of the bvh_node `obj` in preorder, one line per node: "N" for an
+ * interior node, "L a b" for a leaf over children a, b (indices into the
+ * children array given to srr_bvh_node; a == b for a one-child leaf), after a
+ * first line "box minx miny minz maxx maxy maxz".  Returns bytes needed. */
+int64_t srr_bvh_topology(const srr_scene* s, int obj, char* buf, int64_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SRR_CAPI_H */

@@ -1,0 +1,633 @@
+// C-ABI (include/srr_capi.h) and the host render driver: scene upload, the
+// wavefront bounce loop on one HIP stream, batch bookkeeping and timing.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/srr_capi.h"
+#include "kernels.h"
+#include "scene.h"
+
+using namespace srr;
+
+struct srr_scene {
+  Scene s;
+};
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(x)                                                                         \
+  do {                                                                                    \
+    hipError_t e_ = (x);                                                                  \
+    if (e_ != hipSuccess) return fail(SRR_EIO, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+template <class T>
+int upload(T** dst, const std::vector<T>& v) {
+  size_t bytes = std::max<size_t>(v.size() * sizeof(T), 16);
+  HIPCHK(hipMalloc((void**)dst, bytes));
+  if (!v.empty()) HIPCHK(hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  return 0;
+}
+}  // namespace
+
+struct srr_renderer {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[6] = {};  // trace beg/end, frame beg/end, shade beg/end
+  std::vector<void*> scene_bufs;
+  SceneView view{};
+  int n_objs = 0;
+  // path state (capacity cap paths x cap_depth records)
+  size_t cap = 0;
+  int cap_depth = 0;
+  PathState P{};
+  std::vector<void*> path_bufs;
+  int32_t* act[2] = {nullptr, nullptr};
+  int32_t* cnt = nullptr;  // 2 ints
+  uint32_t* ctr = nullptr; // 2 counters (box tests, triangle tests)
+  // frame buffers
+  float* acc = nullptr;
+  size_t acc_cap = 0;
+  int32_t* pixels = nullptr;
+  size_t pix_cap = 0;
+  double* sobol = nullptr;
+  int sobol_n = 0;
+  float* raw_all = nullptr;
+  uint8_t* rays_all = nullptr;
+  size_t keep_cap = 0;
+  int64_t kept_paths = 0;
+  uint64_t last_ctr[2] = {0, 0};
+
+  ~srr_renderer() {
+    if (device >= 0) hipSetDevice(device);
+    for (void* p : scene_bufs) hipFree(p);
+    free_paths();
+    hipFree(act[0]);
+    hipFree(act[1]);
+    hipFree(cnt);
+    hipFree(ctr);
+    hipFree(acc);
+    hipFree(pixels);
+    hipFree(sobol);
+    hipFree(raw_all);
+    hipFree(rays_all);
+    for (hipEvent_t e : ev)
+      if (e) hipEventDestroy(e);
+    if (stream) hipStreamDestroy(stream);
+  }
+  void free_paths() {
+    for (void* p : path_bufs) hipFree(p);
+    path_bufs.clear();
+    cap = 0;
+  }
+  template <class T>
+  int alloc(T** p, size_t n) {
+    HIPCHK(hipMalloc((void**)p, std::max<size_t>(n * sizeof(T), 16)));
+    path_bufs.push_back(*p);
+    return 0;
+  }
+  int ensure_paths(size_t n, int depth, bool keep) {
+    if (n <= cap && depth <= cap_depth && (!keep || P.raw)) return 0;
+    free_paths();
+    hipFree(act[0]);
+    hipFree(act[1]);
+    act[0] = act[1] = nullptr;
+    int d = std::max(depth, 1);
+    if (alloc(&P.ray_o, n) || alloc(&P.ray_d, n) || alloc(&P.lcg, n) || alloc(&P.pcg, n) || alloc(&P.depth, n) ||
+        alloc(&P.spec, n) || alloc(&P.hit_p, n) || alloc(&P.hit_n, n) || alloc(&P.hit_mat, n) ||
+        alloc(&P.rec_a, n * d) || alloc(&P.rec_e, n * d) || alloc(&P.sample, 3 * n))
+      return SRR_ENOMEM;
+    P.raw = nullptr;
+    P.rays = nullptr;
+    if (keep && (alloc(&P.raw, 3 * n) || alloc(&P.rays, n))) return SRR_ENOMEM;
+    HIPCHK(hipMalloc((void**)&act[0], n * sizeof(int32_t)));
+    HIPCHK(hipMalloc((void**)&act[1], n * sizeof(int32_t)));
+    cap = n;
+    cap_depth = d;
+    return 0;
+  }
+};
+
+extern "C" {
+
+const char* srr_last_error(void) { return g_err.c_str(); }
+const char* srr_version(void) { return "srr 0.1 (gfx950 wavefront path tracer)"; }
+
+// ------------------------------------------------------------------ scene
+srr_scene* srr_scene_create(void) { return new srr_scene(); }
+void srr_scene_destroy(srr_scene* s) { delete s; }
+
+int srr_scene_from_text(const char* text, srr_scene** out) {
+  if (!text || !out) return fail(SRR_EINVAL, "null argument");
+  std::unique_ptr<srr_scene> s(new srr_scene());
+  std::string err;
+  int rc = scene_from_text(text, s->s, err);
+  if (rc < 0) return fail(rc, err);
+  *out = s.release();
+  return 0;
+}
+
+int srr_scene_text_handle(const srr_scene* s, int id) {
+  if (!s) return fail(SRR_EINVAL, "null scene");
+  for (auto& kv : s->s.text_ids)
+    if (kv.first == id) return kv.second;
+  return fail(SRR_EINVAL, "no such text object id");
+}
+
+int srr_scene_set_lcg(srr_scene* s, uint64_t state) {
+  if (!s) return fail(SRR_EINVAL, "null scene");
+  s->s.lcg = state & 0xFFFFFFFFFFFFULL;
+  return 0;
+}
+uint64_t srr_scene_get_lcg(const srr_scene* s) { return s ? s->s.lcg : 0; }
+double srr_scene_drand48(srr_scene* s) { return s ? s->s.drand48() : 0.0; }
+
+#define SCN(s) \
+  if (!(s)) return fail(SRR_EINVAL, "null scene");
+#define TEXOK(s, t) \
+  if (!(s)->s.valid_tex(t)) return fail(SRR_EINVAL, "bad texture handle " + std::to_string(t));
+#define MATOK(s, m) \
+  if (!(s)->s.valid_mat(m)) return fail(SRR_EINVAL, "bad material handle " + std::to_string(m));
+#define OBJOK(s, o) \
+  if (!(s)->s.valid_obj(o)) return fail(SRR_EINVAL, "bad hitable handle " + std::to_string(o));
+
+int srr_constant_texture(srr_scene* s, float r, float g, float b) {
+  SCN(s);
+  HTex t;
+  t.kind = TEX_CONST;
+  t.c[0] = r; t.c[1] = g; t.c[2] = b;
+  return s->s.add_tex(std::move(t));
+}
+int srr_image_texture(srr_scene* s, const unsigned char* rgb, int nx, int ny) {
+  SCN(s);
+  if (!rgb || nx <= 0 || ny <= 0) return fail(SRR_EINVAL, "bad image");
+  HTex t;
+  t.kind = TEX_IMAGE;
+  t.nx = nx;
+  t.ny = ny;
+  t.px.assign(rgb, rgb + (size_t)nx * ny * 3);
+  return s->s.add_tex(std::move(t));
+}
+int srr_image_texture_gen(srr_scene* s, int nx, int ny, uint32_t seed, int kind) {
+  SCN(s);
+  if (nx <= 0 || ny <= 0 || kind < 0 || kind > 2) return fail(SRR_EINVAL, "bad image_gen");
+  HTex t;
+  t.kind = TEX_IMAGE;
+  t.nx = nx;
+  t.ny = ny;
+  t.px = gen_image(nx, ny, seed, kind);
+  return s->s.add_tex(std::move(t));
+}
+int srr_checker_texture(srr_scene* s, int even, int odd) {
+  SCN(s);
+  TEXOK(s, even);
+  TEXOK(s, odd);
+  HTex t;
+  t.kind = TEX_CHECKER;
+  t.even = even;
+  t.odd = odd;
+  return s->s.add_tex(std::move(t));
+}
+int srr_noise_texture(srr_scene* s, float scale) {
+  SCN(s);
+  HTex t;
+  t.kind = TEX_NOISE;
+  t.c[0] = scale;
+  return s->s.add_tex(std::move(t));
+}
+
+static int mat_with_tex(srr_scene* s, MatKind k, int tex, float a = 0, float b = 0) {
+  SCN(s);
+  TEXOK(s, tex);
+  float p[4] = {a, b, 0, 0};
+  return s->s.material(k, tex, p);
+}
+int srr_lambertian(srr_scene* s, int t) { return mat_with_tex(s, MAT_LAMBERTIAN, t); }
+int srr_orennayar(srr_scene* s, int t, float sigma) { return mat_with_tex(s, MAT_ORENNAYAR, t, sigma); }
+int srr_beckmann(srr_scene* s, int t, float rx, float ry) { return mat_with_tex(s, MAT_BECKMANN, t, rx, ry); }
+int srr_diffuse_light(srr_scene* s, int t) { return mat_with_tex(s, MAT_DIFFUSE_LIGHT, t); }
+int srr_isotropic(srr_scene* s, int t) { return mat_with_tex(s, MAT_ISOTROPIC, t); }
+int srr_metal(srr_scene* s, float r, float g, float b, float fuzz) {
+  SCN(s);
+  float p[4] = {r, g, b, fuzz};
+  return s->s.material(MAT_METAL, -1, p);
+}
+int srr_dielectric(srr_scene* s, float ri) {
+  SCN(s);
+  float p[4] = {ri, 0, 0, 0};
+  return s->s.material(MAT_DIELECTRIC, -1, p);
+}
+
+int srr_sphere(srr_scene* s, const float c[3], float r, int m) {
+  SCN(s);
+  MATOK(s, m);
+  return s->s.sphere(c, r, m);
+}
+int srr_moving_sphere(srr_scene* s, const float c0[3], const float c1[3], float t0, float t1, float r, int m) {
+  SCN(s);
+  MATOK(s, m);
+  return s->s.moving_sphere(c0, c1, t0, t1, r, m);
+}
+int srr_xy_rect(srr_scene* s, float x0, float x1, float y0, float y1, float k, int m) {
+  SCN(s);
+  MATOK(s, m);
+  return s->s.rect(H_XY, x0, x1, y0, y1, k, m);
+}
+int srr_xz_rect(srr_scene* s, float x0, float x1, float z0, float z1, float k, int m) {
+  SCN(s);
+  MATOK(s, m);
+  return s->s.rect(H_XZ, x0, x1, z0, z1, k, m);
+}
+int srr_yz_rect(srr_scene* s, float y0, float y1, float z0, float z1, float k, int m) {
+  SCN(s);
+  MATOK(s, m);
+  return s->s.rect(H_YZ, y0, y1, z0, z1, k, m);
+}
+int srr_box(srr_scene* s, const float p0[3], const float p1[3], int m) {
+  SCN(s);
+  MATOK(s, m);
+  return s->s.box(p0, p1, m);
+}
+int srr_triangle(srr_scene* s, const float p[9], int m, const float* uv9, const float* n9) {
+  SCN(s);
+  MATOK(s, m);
+  if (!p) return fail(SRR_EINVAL, "null vertices");
+  return s->s.triangle(p, m, uv9, n9);
+}
+int srr_flip_normals(srr_scene* s, int c) {
+  SCN(s);
+  OBJOK(s, c);
+  return s->s.wrap(H_FLIP, c, nullptr);
+}
+int srr_translate(srr_scene* s, int c, const float off[3]) {
+  SCN(s);
+  OBJOK(s, c);
+  return s->s.wrap(H_TRANSLATE, c, off);
+}
+int srr_rotate_y(srr_scene* s, int c, float a) {
+  SCN(s);
+  OBJOK(s, c);
+  return s->s.rotate(H_ROTY, c, a);
+}
+int srr_rotate_x(srr_scene* s, int c, float a) {
+  SCN(s);
+  OBJOK(s, c);
+  return s->s.rotate(H_ROTX, c, a);
+}
+int srr_constant_medium(srr_scene* s, int b, float density, int tex) {
+  SCN(s);
+  OBJOK(s, b);
+  TEXOK(s, tex);
+  return s->s.medium(b, density, tex);
+}
+int srr_hitable_list(srr_scene* s, const int* kids, int n) {
+  SCN(s);
+  if (n < 0 || (n > 0 && !kids)) return fail(SRR_EINVAL, "bad list");
+  for (int i = 0; i < n; ++i) OBJOK(s, kids[i]);
+  return s->s.list(kids, n);
+}
+int srr_bvh_node(srr_scene* s, const int* kids, int n, float t0, float t1) {
+  SCN(s);
+  if (n < 1 || !kids) return fail(SRR_EINVAL, "bvh_node needs n >= 1 children");
+  for (int i = 0; i < n; ++i) OBJOK(s, kids[i]);
+  return s->s.bvh(kids, n, t0, t1);
+}
+int srr_teapot(srr_scene* s, float scale, int divs, int m, int* first) {
+  SCN(s);
+  MATOK(s, m);
+  if (divs < 1 || divs > 400) return fail(SRR_EINVAL, "teapot divs out of range");
+  return s->s.teapot(scale, divs, m, first);
+}
+int srr_camera(srr_scene* s, const float lf[3], const float la[3], const float vup[3], float vfov, float aspect,
+               float aperture, float focus, float t0, float t1) {
+  SCN(s);
+  s->s.camera(lf, la, vup, vfov, aspect, aperture, focus, t0, t1);
+  return 0;
+}
+int srr_scene_set_world(srr_scene* s, int o) {
+  SCN(s);
+  OBJOK(s, o);
+  s->s.world = o;
+  return 0;
+}
+int srr_scene_set_lights(srr_scene* s, int o) {
+  SCN(s);
+  OBJOK(s, o);
+  if (s->s.obj[o].kind != H_LIST) return fail(SRR_EINVAL, "lights must be a hitable_list (Raytracing_n.cpp:75)");
+  s->s.lights = o;
+  return 0;
+}
+
+// --------------------------------------------------------------- renderer
+int srr_renderer_create(const srr_scene* sc, int device, srr_renderer** out) {
+  if (!sc || !out) return fail(SRR_EINVAL, "null argument");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return fail(SRR_ENODEV, "no HIP device (the srr renderer has no CPU fallback)");
+  if (device < 0 || device >= ndev) return fail(SRR_ENODEV, "device index out of range");
+  Flat F;
+  std::string err;
+  int rc = flatten(sc->s, F, err);
+  if (rc < 0) return fail(rc, err);
+  std::unique_ptr<srr_renderer> r(new srr_renderer());
+  r->device = device;
+  HIPCHK(hipSetDevice(device));
+  HIPCHK(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking));
+  for (auto& e : r->ev) HIPCHK(hipEventCreate(&e));
+  auto up = [&](auto** dst, const auto& vec) -> int {
+    int q = upload(dst, vec);
+    if (q == 0) r->scene_bufs.push_back((void*)*dst);
+    return q;
+  };
+  DObj* objs; DXform* xf; DSphere* sph; DRect* rc_; DStandaloneTri* st; DMesh* me; float* nlo; float* nhi;
+  float* tp; TriShade* ts; DMedium* md; DMat* mt; DTex* tx; uint8_t* im; float* pr; int32_t* pp; DLight* li;
+  std::vector<DCamera> cam{F.cam};
+  DCamera* cm;
+  if (up(&objs, F.objs) || up(&xf, F.xforms) || up(&sph, F.spheres) || up(&rc_, F.rects) || up(&st, F.stris) ||
+      up(&me, F.meshes) || up(&nlo, F.node_lo) || up(&nhi, F.node_hi) || up(&tp, F.tri_pos) ||
+      up(&ts, F.tri_shade) || up(&md, F.media) || up(&mt, F.mats) || up(&tx, F.texs) || up(&im, F.images) ||
+      up(&pr, F.perlin_ranvec) || up(&pp, F.perlin_perm) || up(&li, F.lights) || up(&cm, cam))
+    return SRR_EIO;
+  SceneView& V = r->view;
+  V.objs = objs;
+  V.n_world = F.n_world;
+  V.has_media = F.media.empty() ? 0 : 1;
+  V.xforms = xf;
+  V.spheres = sph;
+  V.rects = rc_;
+  V.stris = st;
+  V.meshes = me;
+  V.node_lo = (const float4*)nlo;
+  V.node_hi = (const float4*)nhi;
+  V.tri_pos = (const float4*)tp;
+  V.tri_shade = ts;
+  V.media = md;
+  V.mats = mt;
+  V.texs = tx;
+  V.images = im;
+  V.perlin_ranvec = pr;
+  V.perlin_perm = pp;
+  V.lights = li;
+  V.n_lights = (int)F.lights.size();
+  V.cam = cm;
+  r->n_objs = (int)F.objs.size();
+  HIPCHK(hipMalloc((void**)&r->cnt, 4 * sizeof(int32_t)));
+  HIPCHK(hipMalloc((void**)&r->ctr, 4 * sizeof(uint32_t)));
+  *out = r.release();
+  return 0;
+}
+
+void srr_renderer_destroy(srr_renderer* r) { delete r; }
+
+static bool tile_of(const srr_params* p, int pix) {
+  int tile = p->tile > 0 ? p->tile : 32;
+  int row = pix / p->nx, col = pix % p->nx;
+  int tiles_x = (p->nx + tile - 1) / tile;
+  int t = (row / tile) * tiles_x + col / tile;
+  return (t % p->shard_count) == p->shard_index;
+}
+
+int64_t srr_shard_pixels(const srr_params* p, int32_t* out) {
+  if (!p || p->nx <= 0 || p->ny <= 0 || p->shard_count < 1 || p->shard_index < 0 ||
+      p->shard_index >= p->shard_count)
+    return fail(SRR_EINVAL, "bad params");
+  // shard tiles round-robin; pixels in PPM order within the shard
+  int64_t n = 0;
+  for (int pix = 0; pix < p->nx * p->ny; ++pix)
+    if (p->shard_count == 1 || tile_of(p, pix)) {
+      if (out) out[n] = pix;
+      ++n;
+    }
+  return n;
+}
+
+int srr_render_device(srr_renderer* r, const srr_params* p, float* d_mean, srr_stats* stats) {
+  if (!r || !p || !d_mean) return fail(SRR_EINVAL, "null argument");
+  if (p->spp < 1 || p->max_depth < 0 || p->max_depth > 64) return fail(SRR_EINVAL, "spp >= 1, 0 <= max_depth <= 64");
+  HIPCHK(hipSetDevice(r->device));
+  int64_t npix = srr_shard_pixels(p, nullptr);
+  if (npix < 0) return (int)npix;
+  std::vector<int32_t> pix(npix);
+  srr_shard_pixels(p, pix.data());
+  hipStream_t st = r->stream;
+  bool keep = (p->flags & SRR_FLAG_KEEP_PATHS) != 0;
+  // buffers
+  if ((size_t)npix > r->pix_cap) {
+    hipFree(r->pixels);
+    hipFree(r->acc);
+    HIPCHK(hipMalloc((void**)&r->pixels, npix * sizeof(int32_t)));
+    HIPCHK(hipMalloc((void**)&r->acc, 3 * npix * sizeof(float)));
+    r->pix_cap = npix;
+  }
+  HIPCHK(hipMemcpyAsync(r->pixels, pix.data(), npix * sizeof(int32_t), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemsetAsync(r->acc, 0, 3 * npix * sizeof(float), st));
+  if (p->spp > r->sobol_n) {
+    hipFree(r->sobol);
+    HIPCHK(hipMalloc((void**)&r->sobol, 2 * p->spp * sizeof(double)));
+    r->sobol_n = p->spp;
+  }
+  std::vector<double> sp(2 * (size_t)p->spp);
+  sobol2((unsigned)p->spp, sp.data());
+  HIPCHK(hipMemcpyAsync(r->sobol, sp.data(), sp.size() * sizeof(double), hipMemcpyHostToDevice, st));
+  if (keep) {
+    size_t need = (size_t)npix * p->spp;
+    if (need > r->keep_cap) {
+      hipFree(r->raw_all);
+      hipFree(r->rays_all);
+      HIPCHK(hipMalloc((void**)&r->raw_all, need * 3 * sizeof(float)));
+      HIPCHK(hipMalloc((void**)&r->rays_all, need));
+      r->keep_cap = need;
+    }
+    r->kept_paths = (int64_t)need;
+  }
+  // batch geometry: pixels x samples per batch <= batch_paths
+  int64_t N = p->batch_paths > 0 ? p->batch_paths : (int64_t)1 << 21;
+  int64_t pix_chunk = std::min<int64_t>(npix, N);
+  int S = (int)std::max<int64_t>(1, std::min<int64_t>(p->spp, N / pix_chunk));
+  size_t cap = (size_t)pix_chunk * S;
+  int rc = r->ensure_paths(cap, p->max_depth, keep);
+  if (rc < 0) return rc;
+  if (!keep) { r->P.raw = nullptr; r->P.rays = nullptr; }
+  HIPCHK(hipMemsetAsync(r->ctr, 0, 4 * sizeof(uint32_t), st));
+
+  srr_stats s{};
+  auto t_wall = std::chrono::steady_clock::now();
+  HIPCHK(hipEventRecord(r->ev[2], st));
+  double trace_ms = 0, shade_ms = 0;
+  for (int64_t p0 = 0; p0 < npix; p0 += pix_chunk) {
+    int np = (int)std::min<int64_t>(pix_chunk, npix - p0);
+    for (int s0 = 0; s0 < p->spp; s0 += S) {
+      int Sb = std::min(S, p->spp - s0);
+      BatchInfo B{};
+      B.pixels = r->pixels;
+      B.sobol = r->sobol;
+      B.p0 = (int)p0;
+      B.n_paths = np * Sb;
+      B.s0 = s0;
+      B.spp_batch = Sb;
+      B.nx = p->nx;
+      B.ny = p->ny;
+      B.base_seed = p->base_seed;
+      PathState P = r->P;
+      P.active = r->act[0];
+      launch_raygen(r->view, P, B, st);
+      int n = B.n_paths;
+      HIPCHK(hipMemcpyAsync(r->cnt, &n, sizeof(int), hipMemcpyHostToDevice, st));
+      int cur = 0;
+      for (int bounce = 0; bounce <= p->max_depth && n > 0; ++bounce) {
+        HIPCHK(hipEventRecord(r->ev[0], st));
+        launch_trace(r->view, P, r->act[cur], r->cnt + cur, n, nullptr, st);
+        HIPCHK(hipEventRecord(r->ev[1], st));
+        HIPCHK(hipMemsetAsync(r->cnt + (cur ^ 1), 0, sizeof(int), st));
+        HIPCHK(hipEventRecord(r->ev[4], st));
+        launch_shade(r->view, P, r->act[cur], r->cnt + cur, r->act[cur ^ 1], r->cnt + (cur ^ 1), n, p->max_depth, st);
+        HIPCHK(hipEventRecord(r->ev[5], st));
+        int nn = 0;
+        HIPCHK(hipMemcpyAsync(&nn, r->cnt + (cur ^ 1), sizeof(int), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, r->ev[0], r->ev[1]));
+        trace_ms += ms;
+        HIPCHK(hipEventElapsedTime(&ms, r->ev[4], r->ev[5]));
+        shade_ms += ms;
+        s.world_rays += n;
+        s.trace_launches += 1;
+        s.bounces += 1;
+        n = nn;
+        cur ^= 1;
+      }
+      launch_accumulate(P, B, r->acc, st);
+      if (keep) {
+        // batch paths are [pixel][sample-in-batch]; the frame keeps [pixel][spp]
+        HIPCHK(hipMemcpy2DAsync(r->raw_all + 3 * ((size_t)p0 * p->spp + s0), 3 * sizeof(float) * p->spp, P.raw,
+                                3 * sizeof(float) * Sb, 3 * sizeof(float) * Sb, np, hipMemcpyDeviceToDevice, st));
+        HIPCHK(hipMemcpy2DAsync(r->rays_all + ((size_t)p0 * p->spp + s0), p->spp, P.rays, Sb, Sb, np,
+                                hipMemcpyDeviceToDevice, st));
+      }
+      s.paths += B.n_paths;
+    }
+  }
+  launch_finish(r->acc, d_mean, npix, p->spp, st);
+  HIPCHK(hipEventRecord(r->ev[3], st));
+  HIPCHK(hipStreamSynchronize(st));
+  HIPCHK(hipGetLastError());
+  float total = 0;
+  HIPCHK(hipEventElapsedTime(&total, r->ev[2], r->ev[3]));
+  s.total_ms = total;
+  s.trace_ms = trace_ms;
+  s.shade_ms = shade_ms;
+  (void)t_wall;
+  if (stats) *stats = s;
+  return 0;
+}
+
+int srr_render(srr_renderer* r, const srr_params* p, float* mean, unsigned char* rgb8, srr_stats* stats) {
+  if (!r || !p) return fail(SRR_EINVAL, "null argument");
+  int64_t npix = srr_shard_pixels(p, nullptr);
+  if (npix < 0) return (int)npix;
+  float* d = nullptr;
+  HIPCHK(hipSetDevice(r->device));
+  HIPCHK(hipMalloc((void**)&d, 3 * npix * sizeof(float)));
+  int rc = srr_render_device(r, p, d, stats);
+  std::vector<float> h(3 * npix);
+  if (rc == 0) {
+    hipError_t e = hipMemcpy(h.data(), d, h.size() * sizeof(float), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) rc = fail(SRR_EIO, hipGetErrorString(e));
+  }
+  hipFree(d);
+  if (rc < 0) return rc;
+  if (mean) std::memcpy(mean, h.data(), h.size() * sizeof(float));
+  if (rgb8) srr_tonemap(h.data(), npix, rgb8);
+  return 0;
+}
+
+int srr_copy_paths(srr_renderer* r, float* radiance, unsigned char* rays) {
+  if (!r || !r->raw_all) return fail(SRR_EINVAL, "render with SRR_FLAG_KEEP_PATHS first");
+  HIPCHK(hipSetDevice(r->device));
+  if (radiance) HIPCHK(hipMemcpy(radiance, r->raw_all, r->kept_paths * 3 * sizeof(float), hipMemcpyDeviceToHost));
+  if (rays) HIPCHK(hipMemcpy(rays, r->rays_all, r->kept_paths, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int srr_tonemap(const float* mean, int64_t n, unsigned char* rgb8) {  // Raytracing_n.cpp:850-862
+  if (!mean || !rgb8) return fail(SRR_EINVAL, "null argument");
+  for (int64_t i = 0; i < 3 * n; ++i) {
+    float c = std::sqrt(mean[i]);
+    int q = int(255.99 * c);
+    q = q > 255 ? 255 : q;
+    q = q < 0 ? 0 : q;
+    rgb8[i] = (unsigned char)q;
+  }
+  return 0;
+}
+
+int srr_write_ppm(const char* path, int nx, int ny, const unsigned char* rgb8) {
+  FILE* f = fopen(path, "w");
+  if (!f) return fail(SRR_EIO, std::string("cannot open ") + path);
+  fprintf(f, "P3\n%d %d\n255\n", nx, ny);
+  for (int i = 0; i < nx * ny; ++i) fprintf(f, "%d %d %d\n", rgb8[3 * i], rgb8[3 * i + 1], rgb8[3 * i + 2]);
+  fclose(f);
+  return 0;
+}
+
+int srr_teapot_vertices(float scale, int divs, float* out) {
+  if (divs < 1 || divs > 400) return fail(SRR_EINVAL, "teapot divs out of range");
+  std::vector<float> p;
+  teapot_triangles(scale, divs, p);
+  if (out) std::memcpy(out, p.data(), p.size() * sizeof(float));
+  return (int)(p.size() / 9);
+}
+
+int64_t srr_bvh_topology(const srr_scene* s, int o, char* buf, int64_t cap) {
+  if (!s || !s->s.valid_obj(o) || s->s.obj[o].kind != H_BVH) return fail(SRR_EINVAL, "not a bvh_node handle");
+  const HBvh& B = s->s.bvhs[s->s.obj[o].bvh];
+  std::map<int, int> pos;
+  for (size_t q = 0; q < B.input.size(); ++q) pos[B.input[q]] = (int)q;
+  std::string txt;
+  char line[256];
+  snprintf(line, sizeof line, "box %g %g %g %g %g %g\n", B.box.mn[0], B.box.mn[1], B.box.mn[2], B.box.mx[0],
+           B.box.mx[1], B.box.mx[2]);
+  txt += line;
+  std::vector<int> stack{0};
+  while (!stack.empty()) {
+    int n = stack.back();
+    stack.pop_back();
+    const HBvh::Node& nd = B.nodes[n];
+    if (nd.left < 0) {
+      snprintf(line, sizeof line, "L %d %d\n", pos[B.leaves[~nd.left]], pos[B.leaves[~nd.right]]);
+      txt += line;
+    } else {
+      txt += "N\n";
+      stack.push_back(nd.right);
+      stack.push_back(nd.left);
+    }
+  }
+  if (buf && cap > 0) {
+    int64_t m = std::min<int64_t>(cap - 1, (int64_t)txt.size());
+    std::memcpy(buf, txt.data(), m);
+    buf[m] = 0;
+  }
+  return (int64_t)txt.size() + 1;
+}
+
+int srr_sobol_points(int n, double* out) {
+  if (n < 1 || !out) return fail(SRR_EINVAL, "bad args");
+  sobol2((unsigned)n, out);
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,118 @@
+// Flattened device scene: plain-old-data tables the host flattener
+// (scene.cpp) fills and the HIP kernels (kernels.hip) read.  Layout in HBM:
+//
+//   world objects  DObj[n_world]            the reference's top-level
+//                                           hitable_list, nested lists / boxes
+//                                           inlined in order, instance wrappers
+//                                           distributed onto each child as a
+//                                           transform chain (xforms[])
+//   mesh BVH       float4 node_lo/hi[2*N]   reference-topology BVH2 (bvh.h:96-119):
+//                                           lo = (min.xyz, left), hi = (max.xyz, right);
+//                                           child >= 0 node, < 0 ~triangle
+//   triangles      float4 tri_pos[3*T]      p0, p1, p2 in BVH leaf (DFS) order
+//                  TriShade tri_shade[T]    n0..n2, uv0..uv2, material
+//   materials/textures/images/lights/camera   small tables
+//
+// All indices are 32-bit; a scene is far below 2^31 of anything.
+#pragma once
+#include <cstdint>
+
+namespace srr {
+
+enum ObjKind : int32_t {
+  OBJ_SPHERE = 0,
+  OBJ_MSPHERE = 1,
+  OBJ_RECT = 2,
+  OBJ_TRI = 3,
+  OBJ_MESH = 4,
+  OBJ_MEDIUM = 5,
+};
+
+enum XformKind : int32_t { XF_FLIP = 0, XF_TRANSLATE = 1, XF_ROTY = 2, XF_ROTX = 3 };
+
+struct DXform {  // one instance wrapper (hitable.h:35-203, aarect.h:149-171)
+  int32_t kind;
+  float a, b, c;  // translate: offset; rotate: sin, cos
+};
+
+struct DObj {
+  int32_t kind;
+  int32_t xf_begin, xf_count;  // chain, outermost first
+  int32_t idx;                 // row in the kind's table
+};
+
+struct DSphere {  // sphere.h / moving_sphere.h (static: c1 = c0, t0 = 0, t1 = 1)
+  float c0[3], c1[3];
+  float t0, t1, r;
+  int32_t mat;
+};
+
+struct DRect {  // aarect.h: plane axis kax at k, in-plane axes a0, a1
+  int32_t kax, a0, a1, mat;
+  float lo0, hi0, lo1, hi1, k;
+  float pad[3];
+};
+
+struct TriShade {  // triangle.h fields used after a hit
+  float n[9];      // n0, n1, n2
+  float uv[6];     // uv0.xy, uv1.xy, uv2.xy (uv.z is never read: triangle.h:172-175)
+  int32_t mat;
+};
+
+struct DMesh {
+  int32_t node_off;  // into node arrays (root = node_off)
+  int32_t tri_off;   // into tri arrays
+  int32_t n_nodes, n_tris;
+};
+
+struct DMedium {  // constant_medium.h:4-50
+  int32_t bnd_begin, bnd_count;  // boundary objects (list semantics), in DObj
+  float density;
+  int32_t phase_mat;
+};
+
+enum MatKind : int32_t {
+  MAT_LAMBERTIAN = 0,
+  MAT_ORENNAYAR = 1,
+  MAT_BECKMANN = 2,
+  MAT_METAL = 3,
+  MAT_DIELECTRIC = 4,
+  MAT_DIFFUSE_LIGHT = 5,
+  MAT_ISOTROPIC = 6,
+  MAT_COUNT = 7,
+};
+
+struct DMat {
+  int32_t kind;
+  int32_t tex;       // albedo / emit texture (-1: none)
+  float p[4];        // orennayar: A, B | beckmann: alphax, alphay | metal: rgb, fuzz | dielectric: ri
+};
+
+enum TexKind : int32_t { TEX_CONST = 0, TEX_IMAGE = 1, TEX_CHECKER = 2, TEX_NOISE = 3 };
+
+struct DTex {
+  int32_t kind;
+  int32_t nx, ny;    // image
+  int32_t even, odd; // checker
+  int64_t off;       // image byte offset
+  float c[3];        // const colour; noise: c[0] = scale
+};
+
+enum LightKind : int32_t { LIGHT_NONE = 0, LIGHT_XZRECT = 1, LIGHT_SPHERE = 2, LIGHT_TRI = 3 };
+
+struct DLight {  // hitable_pdf targets (hitable_list.h:54-67)
+  int32_t kind;
+  int32_t idx;   // rect / sphere / standalone-triangle row
+};
+
+struct DCamera {  // camera.h:61-67
+  float origin[3], llc[3], horizontal[3], vertical[3], u[3], v[3];
+  float time0, time1, lens_radius;
+};
+
+struct DStandaloneTri {  // triangle outside any BVH
+  float p[9];
+  TriShade sh;
+};
+
+}  // namespace srr

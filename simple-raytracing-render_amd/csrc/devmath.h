@@ -1,0 +1,87 @@
+// Device math that reproduces the reference's float/double promotions.
+//
+// The reference is compiled C++ on x86-64 (no FMA) linked to glibc's libm.  To
+// track it on gfx950:
+//  * kernels are compiled with -ffp-contract=off (no FMA contraction), and HIP's
+//    default correctly rounded f32 division / sqrt;
+//  * a float libm call of the reference (sinf, cosf, expf, logf, powf, acosf,
+//    asinf, atan2f) is evaluated here in double and rounded once to float:
+//    glibc's float routines are (nearly always) correctly rounded, and so is this;
+//  * double libm calls (sin/cos/log/pow of double) use the device double libm.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace srr {
+namespace dev {
+
+#define SRR_D __device__ __forceinline__
+
+SRR_D float rsin(float x) { return (float)::sin((double)x); }
+SRR_D float rcos(float x) { return (float)::cos((double)x); }
+SRR_D float rexp(float x) { return (float)::exp((double)x); }
+SRR_D float rlog(float x) { return (float)::log((double)x); }
+SRR_D float rpow(float x, float y) { return (float)::pow((double)x, (double)y); }
+SRR_D float racos(float x) { return (float)::acos((double)x); }
+SRR_D float rasin(float x) { return (float)::asin((double)x); }
+SRR_D float ratan2(float y, float x) { return (float)::atan2((double)y, (double)x); }
+SRR_D float rsqrt_exact(float x) { return __fsqrt_rn(x); }  // correctly rounded
+SRR_D float rdiv(float a, float b) { return __fdiv_rn(a, b); }
+
+static constexpr double kPi = 3.14159265358979323846;  // mathf.h:10
+
+// vec3.h: float x3 value type; every operator is the reference's per-component op
+struct V3 {
+  float x, y, z;
+  SRR_D float operator[](int i) const { return i == 0 ? x : (i == 1 ? y : z); }
+  SRR_D void set(int i, float v) {
+    if (i == 0) x = v;
+    else if (i == 1) y = v;
+    else z = v;
+  }
+};
+SRR_D V3 v3(float a, float b, float c) { return V3{a, b, c}; }
+SRR_D V3 v3(float s) { return V3{s, s, s}; }
+SRR_D V3 operator+(V3 a, V3 b) { return V3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+SRR_D V3 operator-(V3 a, V3 b) { return V3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+SRR_D V3 operator-(V3 a) { return V3{-a.x, -a.y, -a.z}; }
+SRR_D V3 operator*(V3 a, V3 b) { return V3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+SRR_D V3 operator*(float t, V3 v) { return V3{t * v.x, t * v.y, t * v.z}; }
+SRR_D V3 operator*(V3 v, float t) { return V3{t * v.x, t * v.y, t * v.z}; }
+SRR_D V3 operator/(V3 v, float t) { return V3{rdiv(v.x, t), rdiv(v.y, t), rdiv(v.z, t)}; }
+SRR_D float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+SRR_D V3 cross(V3 a, V3 b) { return V3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+SRR_D float length(V3 v) { return rsqrt_exact(v.x * v.x + v.y * v.y + v.z * v.z); }
+SRR_D float squared_length(V3 v) { return v.x * v.x + v.y * v.y + v.z * v.z; }
+SRR_D V3 unit_vector(V3 v) { return v / length(v); }
+SRR_D float ffmin(float a, float b) { return a < b ? a : b; }
+SRR_D float ffmax(float a, float b) { return a > b ? a : b; }
+
+struct Ray {  // ray.h
+  V3 o, d;
+  float tm;
+  SRR_D V3 at(float t) const { return o + t * d; }
+};
+
+// mathf.h:14-19 (48-bit LCG) and rng.h:14-35 (PCG32), per path
+struct Rng {
+  uint64_t lcg;
+  uint64_t pcg;
+};
+static constexpr uint64_t kPcgInc = 0xda3e39cb94b95bdbULL;
+SRR_D double drand(Rng& r) {
+  r.lcg = (0x5DEECE66DULL * r.lcg + 0xB16ULL) & 0xFFFFFFFFFFFFULL;
+  return (double)(uint32_t)(r.lcg >> 16) / 4294967296.0;
+}
+SRR_D float pcg_uniform(Rng& r) {
+  uint64_t old = r.pcg;
+  r.pcg = old * 0x5851f42d4c957f2dULL + kPcgInc;
+  uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+  uint32_t rot = (uint32_t)(old >> 59u);
+  uint32_t u = (xs >> rot) | (xs << ((~rot + 1u) & 31));
+  return fminf(0.99999994f, float(u) * 2.3283064365386963e-10f);
+}
+
+}  // namespace dev
+}  // namespace srr

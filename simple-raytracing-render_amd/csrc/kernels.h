@@ -1,0 +1,73 @@
+// Device-side views of the uploaded scene and of the per-path wavefront state,
+// plus the kernel launch shims (kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "device_scene.h"
+
+namespace srr {
+
+struct SceneView {  // device pointers into the flattened tables (device_scene.h)
+  const DObj* objs;
+  int n_world;
+  int has_media;
+  const DXform* xforms;
+  const DSphere* spheres;
+  const DRect* rects;
+  const DStandaloneTri* stris;
+  const DMesh* meshes;
+  const float4* node_lo;
+  const float4* node_hi;
+  const float4* tri_pos;
+  const TriShade* tri_shade;
+  const DMedium* media;
+  const DMat* mats;
+  const DTex* texs;
+  const uint8_t* images;
+  const float* perlin_ranvec;
+  const int32_t* perlin_perm;
+  const DLight* lights;
+  int n_lights;
+  const DCamera* cam;
+};
+
+// Struct-of-arrays state of the paths of one batch (capacity N).
+struct PathState {
+  float4* ray_o;    // origin.xyz, time
+  float4* ray_d;    // direction.xyz
+  uint64_t* lcg;    // 48-bit LCG state (mathf.h:12), per path
+  uint64_t* pcg;    // PCG32 state (pdf.h:20), per path
+  int32_t* depth;   // the reference's *depth
+  uint64_t* spec;   // bit k: bounce k was specular
+  float4* hit_p;    // p.xyz, u
+  float4* hit_n;    // normal.xyz, v
+  int32_t* hit_mat; // material row, -1 null material, -2 miss
+  float4* rec_a;    // [path][max_depth]: attenuation*scattering_pdf (or attenuation), pdf
+  float4* rec_e;    // [path][max_depth]: emitted
+  float* sample;    // [path][3] de_nan'd radiance
+  float* raw;       // [path][3] radiance before de_nan (optional)
+  uint8_t* rays;    // [path] world rays traced (optional)
+  int32_t* active;  // initial active list
+};
+
+struct BatchInfo {
+  const int32_t* pixels;  // shard pixel list (PPM-order indices)
+  const double* sobol;    // [spp][2]
+  int p0;                 // first shard pixel of the batch
+  int n_paths;            // pixels_in_batch * spp_batch
+  int s0, spp_batch;      // sample range [s0, s0 + spp_batch)
+  int nx, ny;
+  uint64_t base_seed;
+};
+
+void launch_raygen(const SceneView& S, const PathState& P, const BatchInfo& B, hipStream_t st);
+void launch_trace(const SceneView& S, const PathState& P, const int* active, const int* count, int max_n,
+                  uint32_t* ctr, hipStream_t st);
+void launch_shade(const SceneView& S, const PathState& P, const int* active, const int* count, int* next,
+                  int* next_count, int max_n, int max_depth, hipStream_t st);
+void launch_accumulate(const PathState& P, const BatchInfo& B, float* acc, hipStream_t st);
+void launch_finish(const float* acc, float* mean, int64_t n, int ns, hipStream_t st);
+
+}  // namespace srr

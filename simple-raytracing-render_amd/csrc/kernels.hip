@@ -1,0 +1,1080 @@
+// srr HIP kernels for gfx950 (MI355X): a wavefront path tracer.
+//
+// One bounce of every live path is one pass over three kernels:
+//   srr_trace  closest hit against the flattened world (the reference's
+//              hitable_list / bvh_node / aabb / triangle / sphere / rect /
+//              constant_medium hit functions) -> SoA hit records     [HOT]
+//   srr_shade  material::scatter + pdf sampling + light pdf (the body of
+//              color(), Raytracing_n.cpp:55-106) -> next ray, or the folded
+//              path radiance; survivors are compacted into the next active
+//              list with one wave-aggregated atomic per wave
+//   (srr_raygen / srr_accumulate / srr_finish around the bounce loop)
+// Semantics follow the reference exactly; see DESIGN.md.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cstdint>
+
+#include "device_scene.h"
+#include "devmath.h"
+#include "kernels.h"
+
+namespace srr {
+namespace dev {
+
+// ===================================================================== hits
+// sphere.h:36-66 and moving_sphere.h:24-51 (static spheres have c1 = c0)
+SRR_D V3 sphere_center(const DSphere& s, float tm, bool moving) {
+  V3 c0 = v3(s.c0[0], s.c0[1], s.c0[2]);
+  if (!moving) return c0;
+  V3 c1 = v3(s.c1[0], s.c1[1], s.c1[2]);
+  return c0 + ((tm - s.t0) / (s.t1 - s.t0)) * (c1 - c0);
+}
+
+SRR_D bool sphere_hit(const DSphere& s, bool moving, const Ray& r, float tmin, float tmax, float& t) {
+  V3 oc = r.o - sphere_center(s, r.tm, moving);
+  float a = dot(r.d, r.d);
+  float b = dot(oc, r.d);
+  float c = dot(oc, oc) - s.r * s.r;
+  float disc = b * b - a * c;
+  if (disc > 0) {
+    float sq = rsqrt_exact(disc);
+    float temp = (-b - sq) / a;
+    if (temp < tmax && temp > tmin) { t = temp; return true; }
+    temp = (-b + sq) / a;
+    if (temp < tmax && temp > tmin) { t = temp; return true; }
+  }
+  return false;
+}
+
+// aarect.h:96-147
+SRR_D bool rect_hit(const DRect& q, const Ray& r, float tmin, float tmax, float& t, float& u, float& v) {
+  float tt = (q.k - r.o[q.kax]) / r.d[q.kax];
+  if (tt < tmin || tt > tmax) return false;
+  float x = r.o[q.a0] + tt * r.d[q.a0];
+  float y = r.o[q.a1] + tt * r.d[q.a1];
+  if (x < q.lo0 || x > q.hi0 || y < q.lo1 || y > q.hi1) return false;
+  u = (x - q.lo0) / (q.hi0 - q.lo0);
+  v = (y - q.lo1) / (q.hi1 - q.lo1);
+  t = tt;
+  return true;
+}
+
+// triangle.h:117-188: two-sided Moller-Trumbore variant on the NORMALISED
+// direction; ignores t_min/t_max and returns a distance.
+SRR_D bool tri_hit(V3 p0, V3 p1, V3 p2, bool front, V3 o, V3 dir, float& t, float& u, float& v) {
+  V3 e1, e2;
+  if (front) { e1 = p1 - p0; e2 = p2 - p0; }
+  else { e1 = p0 - p1; e2 = p2 - p1; }
+  V3 P = cross(dir, e2);
+  float det = dot(e1, P);
+  V3 T;
+  if (det > 0) T = o - p0;
+  else { T = p0 - o; det = -det; }
+  if (det < 0.0001) return false;
+  float uu = dot(T, P);
+  if (uu < 0.0f || uu > det) return false;
+  V3 Q = cross(T, e1);
+  float vv = dot(dir, Q);
+  if (vv < 0.0f || vv + uu > det) return false;
+  float tt = dot(e2, Q);
+  float inv = 1.0f / det;
+  tt *= inv;
+  uu *= inv;
+  vv *= inv;
+  if (tt < 0.0001) return false;
+  t = tt; u = uu; v = vv;
+  return true;
+}
+
+// aabb.h:33-49 with the per-axis reciprocal hoisted (same value each test)
+SRR_D bool slab(float4 lo, float4 hi, V3 o, V3 inv, float tmin, float tmax) {
+#define SRR_AX(A)                                     \
+  {                                                   \
+    float t0 = (lo.A - o.A) * inv.A;                  \
+    float t1 = (hi.A - o.A) * inv.A;                  \
+    if (inv.A < 0.0f) { float s_ = t0; t0 = t1; t1 = s_; } \
+    tmin = t0 > tmin ? t0 : tmin;                     \
+    tmax = t1 < tmax ? t1 : tmax;                     \
+    if (tmax <= tmin) return false;                   \
+  }
+  SRR_AX(x) SRR_AX(y) SRR_AX(z)
+#undef SRR_AX
+  return true;
+}
+
+struct MeshHit {
+  float t;
+  int tri;
+};
+
+// bvh.h:64-93 over the reference-topology BVH: a node is tested against the
+// incoming [tmin, tmax] (never shrunk: the reference tests both children with
+// the same t_max), and among the tested triangles that hit, the smallest t wins,
+// ties to the later DFS leaf (left.t < right.t ? left : right).  Iterative with a
+// short stack; `counters` (optional) tallies box / triangle tests.
+SRR_D bool mesh_hit(const SceneView& S, const DMesh& m, const Ray& r, float tmin, float tmax, bool is_medium,
+                    MeshHit& out, uint32_t* ctr) {
+  V3 inv = v3(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+  V3 dir = r.d / length(r.d);
+  int stack[64];
+  int sp = 0;
+  int node = m.node_off;
+  bool found = false;
+  float best_t = 0;
+  int best_i = -1;
+  uint32_t nbox = 0, ntri = 0;
+  for (;;) {
+    float4 lo = S.node_lo[node];
+    float4 hi = S.node_hi[node];
+    ++nbox;
+    if (slab(lo, hi, r.o, inv, tmin, tmax)) {
+      int L = __float_as_int(lo.w), R = __float_as_int(hi.w);
+      if (L < 0) {
+        // leaf: both children are triangles (L == R for the n == 1 leaf)
+        for (int k = 0; k < 2; ++k) {
+          int ti = ~(k == 0 ? L : R);
+          if (k == 1 && R == L) break;
+          const float4* tp = S.tri_pos + 3 * (size_t)ti;
+          float4 a = tp[0], b = tp[1], c = tp[2];
+          V3 p0 = v3(a.x, a.y, a.z), p1 = v3(b.x, b.y, b.z), p2 = v3(c.x, c.y, c.z);
+          float t, u, v;
+          ++ntri;
+          bool h = tri_hit(p0, p1, p2, true, r.o, dir, t, u, v);
+          if (!h && is_medium) { ++ntri; h = tri_hit(p0, p1, p2, false, r.o, dir, t, u, v); }
+          if (h && (!found || t < best_t || (t == best_t && ti > best_i))) {
+            found = true;
+            best_t = t;
+            best_i = ti;
+          }
+        }
+      } else {
+        if (sp < 64) stack[sp++] = R;
+        node = L;
+        continue;
+      }
+    }
+    if (sp == 0) break;
+    node = stack[--sp];
+  }
+  if (ctr) { atomicAdd(ctr, nbox); atomicAdd(ctr + 1, ntri); }
+  out.t = best_t;
+  out.tri = best_i;
+  return found;
+}
+
+// Instance chain (outermost first): the ray going in (hitable.h:44-52, 109-116,
+// 180-188; flip leaves the ray alone)
+SRR_D Ray chain_in(const SceneView& S, const DObj& ob, Ray r) {
+  for (int k = 0; k < ob.xf_count; ++k) {
+    DXform x = S.xforms[ob.xf_begin + k];
+    if (x.kind == XF_TRANSLATE) r.o = r.o - v3(x.a, x.b, x.c);
+    else if (x.kind == XF_ROTY || x.kind == XF_ROTX) {
+      int ia = x.kind == XF_ROTY ? 0 : 1;
+      float s = x.a, c = x.b;
+      V3 o = r.o, d = r.d;
+      o.set(ia, c * r.o[ia] - s * r.o.z);
+      o.z = s * r.o[ia] + c * r.o.z;
+      d.set(ia, c * r.d[ia] - s * r.d.z);
+      d.z = s * r.d[ia] + c * r.d.z;
+      r.o = o;
+      r.d = d;
+    }
+  }
+  return r;
+}
+
+// ...and the hit record coming out, innermost first
+SRR_D void chain_out(const SceneView& S, const DObj& ob, V3& p, V3& n) {
+  for (int k = ob.xf_count - 1; k >= 0; --k) {
+    DXform x = S.xforms[ob.xf_begin + k];
+    if (x.kind == XF_FLIP) n = -n;
+    else if (x.kind == XF_TRANSLATE) p = p + v3(x.a, x.b, x.c);
+    else {
+      int ia = x.kind == XF_ROTY ? 0 : 1;
+      float s = x.a, c = x.b;
+      V3 pp = p, nn = n;
+      pp.set(ia, c * p[ia] + s * p.z);
+      pp.z = -s * p[ia] + c * p.z;
+      nn.set(ia, c * n[ia] + s * n.z);
+      nn.z = -s * n[ia] + c * n.z;
+      p = pp;
+      n = nn;
+    }
+  }
+}
+
+struct ObjHit {
+  float t;
+  int prim;  // triangle index for meshes
+};
+
+// hit of one non-medium flattened object (in its local frame)
+SRR_D bool basic_hit(const SceneView& S, const DObj& ob, const Ray& lr, float tmin, float tmax, bool is_medium,
+                     ObjHit& h, uint32_t* ctr) {
+  switch (ob.kind) {
+    case OBJ_SPHERE:
+    case OBJ_MSPHERE:
+      return sphere_hit(S.spheres[ob.idx], ob.kind == OBJ_MSPHERE, lr, tmin, tmax, h.t);
+    case OBJ_RECT: {
+      float u, v;
+      return rect_hit(S.rects[ob.idx], lr, tmin, tmax, h.t, u, v);
+    }
+    case OBJ_TRI: {
+      const DStandaloneTri& T = S.stris[ob.idx];
+      V3 p0 = v3(T.p[0], T.p[1], T.p[2]), p1 = v3(T.p[3], T.p[4], T.p[5]), p2 = v3(T.p[6], T.p[7], T.p[8]);
+      V3 dir = lr.d / length(lr.d);
+      float u, v;
+      bool hh = tri_hit(p0, p1, p2, true, lr.o, dir, h.t, u, v);
+      if (!hh && is_medium) hh = tri_hit(p0, p1, p2, false, lr.o, dir, h.t, u, v);
+      return hh;
+    }
+    case OBJ_MESH: {
+      MeshHit mh;
+      if (!mesh_hit(S, S.meshes[ob.idx], lr, tmin, tmax, is_medium, mh, ctr)) return false;
+      h.t = mh.t;
+      h.prim = mh.tri;
+      return true;
+    }
+  }
+  return false;
+}
+
+// hitable_list::hit (hitable_list.h:21-33) over objects [b, b+n) -- used for a
+// medium's boundary (which sees is_medium = true)
+SRR_D bool list_hit(const SceneView& S, int b, int n, const Ray& r, float tmin, float tmax, bool is_medium, float& t,
+                    uint32_t* ctr) {
+  bool any = false;
+  float closest = tmax;
+  for (int k = 0; k < n; ++k) {
+    const DObj& ob = S.objs[b + k];
+    ObjHit h;
+    if (basic_hit(S, ob, chain_in(S, ob, r), tmin, closest, is_medium, h, ctr)) {
+      any = true;
+      closest = h.t;
+      t = h.t;
+    }
+  }
+  return any;
+}
+
+// constant_medium.h:19-50 (two draws, one even on a miss)
+SRR_D bool medium_hit(const SceneView& S, const DMedium& md, const Ray& r, float tmin, float tmax, Rng& rng,
+                      float& t, uint32_t* ctr) {
+  (void)(drand(rng) < 0.00001);
+  float t1, t2;
+  if (list_hit(S, md.bnd_begin, md.bnd_count, r, -FLT_MAX, FLT_MAX, true, t1, ctr)) {
+    if (list_hit(S, md.bnd_begin, md.bnd_count, r, t1 + 0.0001, FLT_MAX, true, t2, ctr)) {
+      if (t1 < tmin) t1 = tmin;
+      if (t2 > tmax) t2 = tmax;
+      if (t1 >= t2) return false;
+      if (t1 < 0) t1 = 0;
+      float len = length(r.d);
+      float inside = (t2 - t1) * len;
+      float hit_distance = -(1 / md.density) * ::log(drand(rng));
+      if (hit_distance < inside) {
+        t = t1 + hit_distance / len;
+        return true;
+      }
+    }
+  }
+  return false;
+}
+
+// The world's hitable_list::hit over the flattened objects, in order; a later
+// object that reports a hit always replaces the record.
+struct WorldHit {
+  int obj;  // -1: miss
+  int prim;
+  float t;
+};
+
+SRR_D WorldHit world_hit(const SceneView& S, const Ray& r, Rng& rng, uint32_t* ctr) {
+  WorldHit w{-1, -1, 0};
+  float closest = FLT_MAX;  // numeric_limits<float>::max(), Raytracing_n.cpp:58
+  const float tmin = 0.001f;
+  for (int k = 0; k < S.n_world; ++k) {
+    const DObj& ob = S.objs[k];
+    Ray lr = chain_in(S, ob, r);
+    ObjHit h;
+    bool hit;
+    if (ob.kind == OBJ_MEDIUM) {
+      hit = medium_hit(S, S.media[ob.idx], lr, tmin, closest, rng, h.t, ctr);
+      h.prim = -1;
+    } else {
+      hit = basic_hit(S, ob, lr, tmin, closest, false, h, ctr);
+    }
+    if (hit) {
+      closest = h.t;
+      w.obj = k;
+      w.prim = h.prim;
+      w.t = h.t;
+    }
+  }
+  return w;
+}
+
+// The winning object's hit record (t, u, v, p, normal, mat), recomputed in its
+// local frame with the same arithmetic as the test, then taken out through the
+// instance chain.
+struct HitRec {
+  V3 p, n;
+  float u, v;
+  int mat;
+};
+
+SRR_D void sphere_uv(V3 p, float& u, float& v) {  // hitable.h:10-15
+  float phi = ratan2(p.z, p.x);
+  float theta = rasin(p.y);
+  u = 1 - (phi + kPi) / (2 * kPi);
+  v = (theta + kPi / 2) / kPi;
+}
+
+SRR_D HitRec world_record(const SceneView& S, const Ray& r, const WorldHit& w) {
+  const DObj& ob = S.objs[w.obj];
+  Ray lr = chain_in(S, ob, r);
+  HitRec h;
+  h.u = 0;  // moving_sphere / constant_medium leave u, v unset in the reference;
+  h.v = 0;  // defined here as 0
+  float t = w.t;
+  switch (ob.kind) {
+    case OBJ_SPHERE:
+    case OBJ_MSPHERE: {
+      const DSphere& s = S.spheres[ob.idx];
+      V3 c = sphere_center(s, lr.tm, ob.kind == OBJ_MSPHERE);
+      h.p = lr.at(t);
+      if (ob.kind == OBJ_SPHERE) sphere_uv((h.p - c) / s.r, h.u, h.v);
+      h.n = (h.p - c) / s.r;
+      h.mat = s.mat;
+      break;
+    }
+    case OBJ_RECT: {
+      const DRect& q = S.rects[ob.idx];
+      float tt;
+      rect_hit(q, lr, -FLT_MAX, FLT_MAX, tt, h.u, h.v);
+      h.p = lr.at(t);
+      h.n = v3(0.f);
+      h.n.set(q.kax, 1.f);
+      h.mat = q.mat;
+      break;
+    }
+    case OBJ_TRI:
+    case OBJ_MESH: {
+      V3 p0, p1, p2;
+      const TriShade* sh;
+      if (ob.kind == OBJ_TRI) {
+        const DStandaloneTri& T = S.stris[ob.idx];
+        p0 = v3(T.p[0], T.p[1], T.p[2]);
+        p1 = v3(T.p[3], T.p[4], T.p[5]);
+        p2 = v3(T.p[6], T.p[7], T.p[8]);
+        sh = &T.sh;
+      } else {
+        const float4* tp = S.tri_pos + 3 * (size_t)w.prim;
+        float4 a = tp[0], b = tp[1], c = tp[2];
+        p0 = v3(a.x, a.y, a.z);
+        p1 = v3(b.x, b.y, b.z);
+        p2 = v3(c.x, c.y, c.z);
+        sh = &S.tri_shade[w.prim];
+      }
+      V3 dir = lr.d / length(lr.d);
+      float tt, u, v;
+      tri_hit(p0, p1, p2, true, lr.o, dir, tt, u, v);  // world rays never take the back test
+      float a0 = 1 - u - v;
+      // triangle.h:172-184
+      float uvx = a0 * sh->uv[0] + u * sh->uv[2] + v * sh->uv[4];
+      float uvy = a0 * sh->uv[1] + u * sh->uv[3] + v * sh->uv[5];
+      h.u = uvx;
+      h.v = uvy;
+      V3 n0 = v3(sh->n[0], sh->n[1], sh->n[2]), n1 = v3(sh->n[3], sh->n[4], sh->n[5]),
+         n2 = v3(sh->n[6], sh->n[7], sh->n[8]);
+      h.n = unit_vector(a0 * n0 + u * n1 + v * n2);
+      h.p = a0 * p0 + u * p1 + v * p2;
+      h.mat = sh->mat;
+      break;
+    }
+    case OBJ_MEDIUM: {
+      h.p = lr.at(t);
+      h.n = v3(1, 0, 0);
+      h.mat = S.media[ob.idx].phase_mat;
+      break;
+    }
+  }
+  chain_out(S, ob, h.p, h.n);
+  return h;
+}
+
+// ================================================================ shading
+SRR_D V3 tex_value(const SceneView& S, int ti, float u, float v, V3 p) {
+  // checker_texture recursion (texture.h:13-19) unrolled to a few levels
+  for (int guard = 0; guard < 8; ++guard) {
+    const DTex& T = S.texs[ti];
+    if (T.kind == TEX_CONST) return v3(T.c[0], T.c[1], T.c[2]);
+    if (T.kind == TEX_IMAGE) {  // texture.h:58-70
+      int i = (u) * T.nx;
+      int j = (1 - v) * T.ny - 0.001;
+      if (i < 0) i = 0;
+      if (j < 0) j = 0;
+      if (i > T.nx - 1) i = T.nx - 1;
+      if (j > T.ny - 1) j = T.ny - 1;
+      const uint8_t* px = S.images + T.off + 3 * (size_t)i + 3 * (size_t)T.nx * j;
+      float r = int(px[0]) / 255.0;
+      float g = int(px[1]) / 255.0;
+      float b = int(px[2]) / 255.0;
+      return v3(r, g, b);
+    }
+    if (T.kind == TEX_CHECKER) {
+      float sines = rsin(10 * p.x) * rsin(10 * p.y) * rsin(10 * p.z);
+      ti = sines < 0 ? T.odd : T.even;
+      continue;
+    }
+    // noise_texture (texture.h:35-46) with perlin.h's turb()
+    float scale = T.c[0];
+    V3 tp = scale * p;
+    float accum = 0, weight = 1.0f;
+    for (int oct = 0; oct < 7; ++oct) {
+      float fx = floorf(tp.x), fy = floorf(tp.y), fz = floorf(tp.z);
+      float uu = tp.x - fx, vv = tp.y - fy, ww = tp.z - fz;
+      int i = (int)fx, j = (int)fy, k = (int)fz;
+      float hu = uu * uu * (3 - 2 * uu), hv = vv * vv * (3 - 2 * vv), hw = ww * ww * (3 - 2 * ww);
+      float acc = 0;
+      for (int a = 0; a < 2; a++)
+        for (int b = 0; b < 2; b++)
+          for (int c = 0; c < 2; c++) {
+            int idx = S.perlin_perm[(i + a) & 255] ^ S.perlin_perm[256 + ((j + b) & 255)] ^
+                      S.perlin_perm[512 + ((k + c) & 255)];
+            V3 g = v3(S.perlin_ranvec[3 * idx], S.perlin_ranvec[3 * idx + 1], S.perlin_ranvec[3 * idx + 2]);
+            V3 wv = v3(uu - a, vv - b, ww - c);
+            acc += (a * hu + (1 - a) * (1 - hu)) * (b * hv + (1 - b) * (1 - hv)) * (c * hw + (1 - c) * (1 - hw)) *
+                   dot(g, wv);
+          }
+      accum += weight * acc;
+      weight *= 0.5f;
+      tp = tp * 2.0f;
+    }
+    float turb = fabsf(accum);
+    return v3(1, 1, 1) * 0.5f * (1 + rsin(scale * p.z + 5 * turb));
+  }
+  return v3(0.f);
+}
+
+struct Onb {  // onb.h:21-30
+  V3 u, v, w;
+};
+SRR_D Onb onb_from_w(V3 n) {
+  Onb o;
+  o.w = unit_vector(n);
+  V3 a = (fabsf(o.w.x) > 0.9) ? v3(0, 1, 0) : v3(1, 0, 0);
+  o.v = unit_vector(cross(o.w, a));
+  o.u = cross(o.w, o.v);
+  return o;
+}
+SRR_D V3 onb_local(const Onb& b, V3 a) { return a.x * b.u + a.y * b.v + a.z * b.w; }
+
+// reflection.h:8-32
+SRR_D float Cos2Theta(V3 w) { return w.z * w.z; }
+SRR_D float AbsCosTheta(V3 w) { return fabsf(w.z); }
+SRR_D float Sin2Theta(V3 w) { return fmaxf(0.0f, 1.0f - Cos2Theta(w)); }
+SRR_D float SinTheta(V3 w) { return rsqrt_exact(Sin2Theta(w)); }
+SRR_D float TanTheta(V3 w) { return SinTheta(w) / w.z; }
+SRR_D float Tan2Theta(V3 w) { return Sin2Theta(w) / Cos2Theta(w); }
+SRR_D float clamp11(float x) { return x < -1 ? -1.f : (x > 1 ? 1.f : x); }
+SRR_D float CosPhi(V3 w) {
+  float s = SinTheta(w);
+  return (s == 0) ? 1 : clamp11(w.x / s);
+}
+SRR_D float SinPhi(V3 w) {
+  float s = SinTheta(w);
+  return (s == 0) ? 0 : clamp11(w.y / s);
+}
+SRR_D float Cos2Phi(V3 w) { return CosPhi(w) * CosPhi(w); }
+SRR_D float Sin2Phi(V3 w) { return SinPhi(w) * SinPhi(w); }
+
+// common.h:26-78
+SRR_D float Erf(float x) {
+  float a1 = 0.254829592f, a2 = -0.284496736f, a3 = 1.421413741f, a4 = -1.453152027f, a5 = 1.061405429f;
+  float p = 0.3275911f;
+  int sign = 1;
+  if (x < 0) sign = -1;
+  x = fabsf(x);
+  float t = 1 / (1 + p * x);
+  float y = 1 - (((((a5 * t + a4) * t) + a3) * t + a2) * t + a1) * t + rexp(-x * x);
+  return sign * y;
+}
+SRR_D float ErfInv(float x) {
+  float w, p;
+  x = x < -.99999f ? -.99999f : (x > .99999f ? .99999f : x);
+  w = -rlog((1 - x) * (1 + x));
+  if (w < 5) {
+    w = w - 2.5f;
+    p = 2.81022636e-08f;
+    p = 3.43273939e-07f + p * w;
+    p = -3.5233877e-06f + p * w;
+    p = -4.39150654e-06f + p * w;
+    p = 0.00021858087f + p * w;
+    p = -0.00125372503f + p * w;
+    p = -0.00417768164f + p * w;
+    p = 0.246640727f + p * w;
+    p = 1.50140941f + p * w;
+  } else {
+    w = rsqrt_exact(w) - 3;
+    p = -0.000200214257f;
+    p = 0.000100950558f + p * w;
+    p = 0.00134934322f + p * w;
+    p = -0.00367342844f + p * w;
+    p = 0.00573950773f + p * w;
+    p = -0.0076224613f + p * w;
+    p = 0.00943887047f + p * w;
+    p = 1.00167406f + p * w;
+    p = 2.83297682f + p * w;
+  }
+  return p * x;
+}
+
+// microfacet_distribution.h:137-211, sampleVisibleArea = true
+struct Beck {
+  float ax, ay;
+  SRR_D float D(V3 wh) const {
+    float tan2 = Tan2Theta(wh);
+    if (isinf(tan2)) return 0.;
+    float cos4 = Cos2Theta(wh) * Cos2Theta(wh);
+    return rexp(-tan2 * (Cos2Phi(wh) / (ax * ax) + Sin2Phi(wh) / (ay * ay))) / (kPi * ax * ay * cos4);
+  }
+  SRR_D float Lambda(V3 w) const {
+    float absTan = fabsf(TanTheta(w));
+    if (isinf(absTan)) return 0;
+    float alpha = rsqrt_exact(Cos2Phi(w) * ax * ax + Sin2Phi(w) * ay * ay);
+    float a = 1 / (alpha * absTan);
+    if (a > 1.6f) return 0;
+    return (1 - 1.259f * a + 0.396f * a * a) / (3.535f * a + 2.181f * a * a);
+  }
+  SRR_D float G1(V3 w) const { return 1 / (1 + Lambda(w)); }
+  SRR_D float G(V3 wo, V3 wi) const { return 1 / (1 + Lambda(wo) + Lambda(wi)); }
+  SRR_D float Pdf(V3 wo, V3 wh) const { return D(wh) * G1(wo) * fabsf(dot(wo, wh)) / AbsCosTheta(wo); }
+};
+
+SRR_D void beckmann_sample11(float cosThetaI, float u1, float u2, float& sx, float& sy) {  // :34-107
+  if (cosThetaI > .9999) {
+    float r = rsqrt_exact(-rlog(1.0f - u1));
+    float sinPhi = ::sin(2 * kPi * u2);
+    float cosPhi = ::cos(2 * kPi * u2);
+    sx = r * cosPhi;
+    sy = r * sinPhi;
+    return;
+  }
+  float sinThetaI = rsqrt_exact(fmaxf(0.0f, 1.0f - cosThetaI * cosThetaI));
+  float tanThetaI = sinThetaI / cosThetaI;
+  float cotThetaI = 1 / tanThetaI;
+  float a = -1, c = Erf(cosThetaI);
+  float sample_x = fmaxf(u1, 1e-6f);
+  float thetaI = racos(cosThetaI);
+  float fit = 1 + thetaI * (-0.876f + thetaI * (0.4265f - 0.0594f * thetaI));
+  float b = c - (1 + c) * rpow(1 - sample_x, fit);
+  const float SQRT_PI_INV = (float)(1.f / ::sqrt(kPi));
+  float normalization = 1 / (1 + c + SQRT_PI_INV * tanThetaI * rexp(-cotThetaI * cotThetaI));
+  int it = 0;
+  while (++it < 10) {
+    if (!(b >= a && b <= c)) b = 0.5f * (a + c);
+    float invErf = ErfInv(b);
+    float value = normalization * (1 + b + SQRT_PI_INV * tanThetaI * (rexp(-invErf * invErf))) - sample_x;
+    float derivative = normalization * (1 - invErf * tanThetaI);
+    if (fabsf(value) < 1e-5f) break;
+    if (value > 0) c = b;
+    else a = b;
+    b -= value / derivative;
+  }
+  sx = ErfInv(b);
+  sy = ErfInv(2.0f * fmaxf(u2, 1e-6f) - 1.0f);
+}
+
+SRR_D V3 beckmann_sample_wh(const Beck& d, V3 wo, float u1, float u2) {  // :12-32, :203-210
+  bool flip = wo.z < 0;
+  V3 wi = flip ? -wo : wo;
+  V3 ws = unit_vector(v3(d.ax * wi.x, d.ay * wi.y, wi.z));
+  float sx, sy;
+  beckmann_sample11(ws.z, u1, u2, sx, sy);
+  float tmp = CosPhi(ws) * sx - SinPhi(ws) * sy;
+  sy = SinPhi(ws) * sx + CosPhi(ws) * sy;
+  sx = tmp;
+  sx = d.ax * sx;
+  sy = d.ay * sy;
+  V3 wh = unit_vector(v3(-sx, -sy, 1.f));
+  if (flip) wh = -wh;
+  return wh;
+}
+
+// pdf.h:10-18
+SRR_D V3 random_cosine_direction(Rng& rng) {
+  float r1 = drand(rng);
+  float r2 = drand(rng);
+  float phi = 2 * kPi * r1;
+  float z = rsqrt_exact(1 - r2);
+  float x = rcos(phi) * 2 * rsqrt_exact(r2);
+  float y = rsin(phi) * 2 * rsqrt_exact(r2);
+  return v3(x, y, z);
+}
+
+// material.h:43-50: the three draws land in z, y, x (g++ argument order)
+SRR_D V3 random_in_unit_sphere(Rng& rng) {
+  V3 p;
+  do {
+    float z = (float)drand(rng);
+    float y = (float)drand(rng);
+    float x = (float)drand(rng);
+    p = 2.0f * v3(x, y, z) - v3(1, 1, 1);
+  } while (dot(p, p) >= 1.0);
+  return p;
+}
+
+// light list (hitable_pdf over a hitable_list, hitable_list.h:54-67)
+SRR_D float light_pdf_one(const SceneView& S, const DLight& L, V3 o, V3 v) {
+  Ray r{o, v, 0.0f};
+  if (L.kind == LIGHT_XZRECT) {  // aarect.h:45-55
+    const DRect& q = S.rects[L.idx];
+    float t, u, vv;
+    if (rect_hit(q, r, 0.001f, FLT_MAX, t, u, vv)) {
+      float area = (q.hi0 - q.lo0) * (q.hi1 - q.lo1);
+      float distance_square = t * t * squared_length(v);
+      float cosine = fabsf(v.y / length(v));  // dot(v, (0,1,0)) / |v|
+      return distance_square / (cosine * area);
+    }
+    return 0;
+  }
+  if (L.kind == LIGHT_SPHERE) {  // sphere.h:69-78
+    const DSphere& s = S.spheres[L.idx];
+    float t;
+    if (sphere_hit(s, false, r, 0.001f, FLT_MAX, t)) {
+      V3 c = v3(s.c0[0], s.c0[1], s.c0[2]);
+      float cos_theta_max = rsqrt_exact(1 - s.r * s.r / squared_length(c - o));
+      float solid_angle = 2 * kPi * (1 - cos_theta_max);
+      return 1 / solid_angle;
+    }
+    return 0;
+  }
+  if (L.kind == LIGHT_TRI) {  // triangle.h:70-87
+    const DStandaloneTri& T = S.stris[L.idx];
+    V3 p0 = v3(T.p[0], T.p[1], T.p[2]), p1 = v3(T.p[3], T.p[4], T.p[5]), p2 = v3(T.p[6], T.p[7], T.p[8]);
+    float t, u, vv;
+    if (tri_hit(p0, p1, p2, true, o, v / length(v), t, u, vv)) {
+      const TriShade& sh = T.sh;
+      float a0 = 1 - u - vv;
+      V3 n = unit_vector(a0 * v3(sh.n[0], sh.n[1], sh.n[2]) + u * v3(sh.n[3], sh.n[4], sh.n[5]) +
+                         vv * v3(sh.n[6], sh.n[7], sh.n[8]));
+      V3 v01 = p1 - p0;
+      V3 v01n = v01 / length(v01);
+      V3 v02 = p2 - p0;
+      V3 v02n = v02 / length(v02);
+      float cos102 = dot(v01n, v02n);
+      float sin102 = rsqrt_exact(1 - cos102 * cos102);
+      float h = length(v02) * sin102;
+      float area = 0.5 * length(v01) * h;
+      float distance_square = t * t * squared_length(v);
+      float cosine = fabsf(dot(v, n)) / length(v);
+      return distance_square / (cosine * area);
+    }
+    return 0;
+  }
+  return 0.0;
+}
+
+SRR_D float lights_pdf(const SceneView& S, V3 o, V3 v) {
+  float weight = 1.0 / S.n_lights;
+  float sum = 0;
+  for (int k = 0; k < S.n_lights; ++k) sum += weight * light_pdf_one(S, S.lights[k], o, v);
+  return sum;
+}
+
+SRR_D V3 lights_random(const SceneView& S, V3 o, Rng& rng) {
+  int index = int(drand(rng) * S.n_lights);
+  const DLight& L = S.lights[index];
+  if (L.kind == LIGHT_XZRECT) {  // aarect.h:57-60: z drawn before x
+    const DRect& q = S.rects[L.idx];
+    float z = q.lo1 + drand(rng) * (q.hi1 - q.lo1);
+    float x = q.lo0 + drand(rng) * (q.hi0 - q.lo0);
+    return v3(x, q.k, z) - o;
+  }
+  if (L.kind == LIGHT_SPHERE) {  // sphere.h:7-15, 80-86
+    const DSphere& s = S.spheres[L.idx];
+    V3 dirc = v3(s.c0[0], s.c0[1], s.c0[2]) - o;
+    float d2 = squared_length(dirc);
+    Onb uvw = onb_from_w(dirc);
+    float r1 = drand(rng);
+    float r2 = drand(rng);
+    float z = 1 + r2 * (rsqrt_exact(1 - s.r * s.r / d2) - 1);
+    float phi = 2 * kPi * r1;
+    float x = rcos(phi) * rsqrt_exact(1 - z * z);
+    float y = rsin(phi) * rsqrt_exact(1 - z * z);
+    return onb_local(uvw, v3(x, y, z));
+  }
+  if (L.kind == LIGHT_TRI) {  // triangle.h:89-94
+    const DStandaloneTri& T = S.stris[L.idx];
+    float u = drand(rng);
+    float v = drand(rng) * (1 - u);
+    V3 p0 = v3(T.p[0], T.p[1], T.p[2]), p1 = v3(T.p[3], T.p[4], T.p[5]), p2 = v3(T.p[6], T.p[7], T.p[8]);
+    return p0 * (1 - u - v) + p1 * u + p2 * v - o;
+  }
+  return v3(1, 0, 0);
+}
+
+// The BSDF half of the mixture (pdf.h:30-156) for one non-specular hit.
+struct Bsdf {
+  int kind;
+  Onb uvw;
+  V3 n;
+  float A, B;      // orennayar
+  Beck dist;       // beckmann
+  float beck_pdf;  // beckmann_pdf::pdf_value, set by generate (starts 0)
+};
+
+SRR_D V3 to_local_unit(const Onb& b, V3 d) {
+  V3 ud = unit_vector(d);
+  return unit_vector(v3(dot(ud, b.u), dot(ud, b.v), dot(ud, b.w)));
+}
+
+SRR_D V3 bsdf_generate(Bsdf& f, V3 wo, Rng& rng) {
+  if (f.kind == MAT_BECKMANN) {  // pdf.h:136-152
+    float u1 = pcg_uniform(rng);
+    float u2 = pcg_uniform(rng);
+    V3 mwo = -wo;
+    V3 wwo = unit_vector(v3(dot(mwo, f.uvw.u), dot(mwo, f.uvw.v), dot(mwo, f.uvw.w)));
+    V3 wh = beckmann_sample_wh(f.dist, wwo, u1, u2);
+    V3 uw = unit_vector(wwo);
+    V3 wi = -uw + 2 * dot(uw, wh) * wh;  // Reflect (reflection.h:34-36)
+    V3 wwi = unit_vector(wi.x * f.uvw.u + wi.y * f.uvw.v + wi.z * f.uvw.w);
+    f.beck_pdf = f.dist.D(wh) * f.dist.G(wo, wi) / (4 * AbsCosTheta(wi) * AbsCosTheta(wwo));
+    if (!(wi.z * wwo.z > 0)) f.beck_pdf = 0;
+    return wwi;
+  }
+  // cosine_pdf / onrennayar_pdf (pdf.h:47-56, 103-112)
+  V3 g = random_cosine_direction(rng);
+  if (dot(-wo, f.n) > 0) g.z *= -1;
+  return onb_local(f.uvw, g);
+}
+
+SRR_D float bsdf_value(const Bsdf& f, V3 wo, V3 wi) {
+  if (f.kind == MAT_BECKMANN) return f.beck_pdf;
+  if (f.kind == MAT_LAMBERTIAN) {  // pdf.h:33-46
+    float co = dot(unit_vector(wo), f.n);
+    float ci = dot(unit_vector(wi), f.n);
+    if (ci * co < 0) return fabsf(ci) / kPi;
+    return 0;
+  }
+  // onrennayar_pdf::value (pdf.h:64-101)
+  V3 lo = to_local_unit(f.uvw, -wo);
+  V3 li = to_local_unit(f.uvw, wi);
+  float sinThetaI = SinTheta(li), sinThetaO = SinTheta(lo);
+  float maxCos = 0;
+  if (sinThetaI > 1e-4 && sinThetaO > 1e-4) {
+    float sinPhiI = SinPhi(li), cosPhiI = CosPhi(li);
+    float sinPhiO = SinPhi(lo), cosPhiO = CosPhi(lo);
+    float dCos = cosPhiI * cosPhiO + sinPhiI * sinPhiO;
+    maxCos = ffmax(0.0f, dCos);
+  }
+  float sinAlpha, tanBeta;
+  if (AbsCosTheta(li) > AbsCosTheta(lo)) {
+    sinAlpha = sinThetaO;
+    tanBeta = sinThetaI / AbsCosTheta(li);
+  } else {
+    sinAlpha = sinThetaI;
+    tanBeta = sinThetaO / AbsCosTheta(lo);
+  }
+  float cosine = li.z;
+  if (cosine < 0) cosine = 0;
+  return cosine * (f.A + f.B * maxCos * sinAlpha * tanBeta) / kPi;
+}
+
+SRR_D float scattering_pdf(const Bsdf& f, V3 n, V3 rin, V3 sc) {
+  if (f.kind == MAT_BECKMANN) {  // material.h:160-185
+    V3 wo = to_local_unit(f.uvw, -rin);
+    V3 wi = to_local_unit(f.uvw, sc);
+    V3 wh = unit_vector(wi + wo);
+    return f.dist.Pdf(wo, wh) / (4 * dot(wo, wh));
+  }
+  float c = dot(n, unit_vector(sc));  // material.h:100-105, 134-138
+  if (c < 0) c = 0;
+  return c / kPi;
+}
+
+// ================================================================ kernels
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+// Wave-aggregated append: one atomic per wave for the lanes with `pred`.
+__device__ __forceinline__ void append(bool pred, int value, int* list, int* count) {
+  uint64_t mask = __ballot(pred);
+  if (!mask) return;
+  int leader = __ffsll((unsigned long long)mask) - 1;
+  int base = 0;
+  if (lane_id() == leader) base = atomicAdd(count, __popcll(mask));
+  base = __shfl(base, leader);
+  if (pred) {
+    int rank = __popcll(mask & ((1ull << lane_id()) - 1));
+    list[base + rank] = value;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_raygen(SceneView S, PathState P, BatchInfo B) {
+  int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= B.n_paths) return;
+  int lp = p / B.spp_batch;
+  int s = B.s0 + p % B.spp_batch;
+  int pix = B.pixels[B.p0 + lp];
+  int i = pix % B.nx;
+  int j = B.ny - 1 - pix / B.nx;  // Raytracing_n.cpp:827-828 (SURVEY Q12 fix)
+  // per-path seeding
+  uint64_t h = 0xcbf29ce484222325ULL ^ B.base_seed;
+  uint32_t w[3] = {(uint32_t)i, (uint32_t)j, (uint32_t)s};
+  for (int k = 0; k < 3; ++k)
+    for (int b = 0; b < 4; ++b) {
+      h ^= (w[k] >> (8 * b)) & 0xffu;
+      h *= 0x100000001b3ULL;
+    }
+  Rng rng;
+  rng.lcg = h & 0xFFFFFFFFFFFFULL;
+  rng.pcg = 0x853c49e6748fea9bULL ^ (rng.lcg << 16);
+  // Raytracing_n.cpp:834-836 and camera::get_ray (camera.h:51-59)
+  float u = float(B.sobol[2 * s] + i) / float(B.nx);
+  float v = float(B.sobol[2 * s + 1] + j) / float(B.ny);
+  const DCamera& C = *S.cam;
+  V3 pd;
+  do {  // random_in_unit_disk (camera.h:8-14): y drawn before x
+    float y = drand(rng);
+    float x = drand(rng);
+    pd = 2.0f * v3(x, y, 0) - v3(1, 1, 0);
+  } while (dot(pd, pd) >= 1.0);
+  V3 rd = C.lens_radius * pd;
+  V3 cu = v3(C.u[0], C.u[1], C.u[2]), cv = v3(C.v[0], C.v[1], C.v[2]);
+  V3 offset = cu * rd.x + cv * rd.y;
+  float time = C.time0 + drand(rng) * (C.time1 - C.time0);
+  V3 org = v3(C.origin[0], C.origin[1], C.origin[2]);
+  V3 dir = v3(C.llc[0], C.llc[1], C.llc[2]) + u * v3(C.horizontal[0], C.horizontal[1], C.horizontal[2]) +
+           v * v3(C.vertical[0], C.vertical[1], C.vertical[2]) - org - offset;
+  dir = unit_vector(dir);
+  V3 o = org + offset;
+  P.ray_o[p] = make_float4(o.x, o.y, o.z, time);
+  P.ray_d[p] = make_float4(dir.x, dir.y, dir.z, 0.f);
+  P.lcg[p] = rng.lcg;
+  P.pcg[p] = rng.pcg;
+  P.depth[p] = 0;
+  P.spec[p] = 0;
+  P.active[p] = p;
+  if (P.rays) P.rays[p] = 0;
+}
+
+__global__ void __launch_bounds__(256) k_trace(SceneView S, PathState P, const int* active, const int* count,
+                                               uint32_t* ctr) {
+  int q = blockIdx.x * blockDim.x + threadIdx.x;
+  int n = *count;
+  if (q >= n) return;
+  int p = active[q];
+  float4 ro = P.ray_o[p], rdv = P.ray_d[p];
+  Ray r{v3(ro.x, ro.y, ro.z), v3(rdv.x, rdv.y, rdv.z), ro.w};
+  Rng rng{P.lcg[p], P.pcg[p]};
+  WorldHit w = world_hit(S, r, rng, ctr);
+  if (S.has_media) P.lcg[p] = rng.lcg;
+  if (w.obj < 0) {
+    P.hit_mat[p] = -2;
+    return;
+  }
+  HitRec h = world_record(S, r, w);
+  P.hit_p[p] = make_float4(h.p.x, h.p.y, h.p.z, h.u);
+  P.hit_n[p] = make_float4(h.n.x, h.n.y, h.n.z, h.v);
+  P.hit_mat[p] = h.mat;
+}
+
+// Folds the recorded bounces back to front exactly like the recursion returns
+// (Raytracing_n.cpp:69 and :94), then de_nan and store the sample.
+__device__ void finish_path(const PathState& P, int p, V3 C, int depth, uint64_t spec, int max_depth) {
+  for (int k = depth - 1; k >= 0; --k) {
+    float4 a = P.rec_a[(size_t)p * max_depth + k];
+    V3 av = v3(a.x, a.y, a.z);
+    if ((spec >> k) & 1) {
+      C = av * C;
+    } else {
+      float4 e = P.rec_e[(size_t)p * max_depth + k];
+      C = v3(e.x, e.y, e.z) + (av * C) / a.w;
+    }
+  }
+  if (P.raw) {
+    P.raw[3 * (size_t)p] = C.x;
+    P.raw[3 * (size_t)p + 1] = C.y;
+    P.raw[3 * (size_t)p + 2] = C.z;
+  }
+  // de_nan (Raytracing_n.cpp:47-53)
+  if (!(C.x == C.x)) C.x = 0;
+  if (!(C.y == C.y)) C.y = 0;
+  if (!(C.z == C.z)) C.z = 0;
+  P.sample[3 * (size_t)p] = C.x;
+  P.sample[3 * (size_t)p + 1] = C.y;
+  P.sample[3 * (size_t)p + 2] = C.z;
+}
+
+__global__ void __launch_bounds__(256) k_shade(SceneView S, PathState P, const int* active, const int* count,
+                                               int* next, int* next_count, int max_depth) {
+  int q = blockIdx.x * blockDim.x + threadIdx.x;
+  int n = *count;
+  bool alive = false;
+  int p = -1;
+  if (q < n) {
+    p = active[q];
+    float4 ro = P.ray_o[p], rdv = P.ray_d[p];
+    V3 rdir = v3(rdv.x, rdv.y, rdv.z);
+    int depth = P.depth[p];
+    uint64_t spec = P.spec[p];
+    if (P.rays) P.rays[p] += 1;
+    int mat = P.hit_mat[p];
+    if (mat < 0) {
+      // miss -> vec3(0.0) (:104); a null material* is UB in the reference: 0 here
+      finish_path(P, p, v3(0.f), depth, spec, max_depth);
+    } else {
+      float4 hp = P.hit_p[p], hn = P.hit_n[p];
+      V3 hpt = v3(hp.x, hp.y, hp.z), nrm = v3(hn.x, hn.y, hn.z);
+      float hu = hp.w, hv = hn.w;
+      const DMat M = S.mats[mat];
+      V3 emitted = v3(0.f);
+      if (M.kind == MAT_DIFFUSE_LIGHT && dot(nrm, rdir) < 0.0)  // material.h:348-354
+        emitted = tex_value(S, M.tex, hu, hv, hpt);
+      if (depth < max_depth && M.kind != MAT_DIFFUSE_LIGHT) {
+        Rng rng{P.lcg[p], P.pcg[p]};
+        V3 ndir;
+        float ntime = 0.0f;  // ray(a, b) defaults time to 0 (ray.h:10) for specular rays
+        size_t slot = (size_t)p * max_depth + depth;
+        if (M.kind == MAT_METAL || M.kind == MAT_DIELECTRIC || M.kind == MAT_ISOTROPIC) {
+          V3 atten;
+          if (M.kind == MAT_METAL) {  // material.h:248-256
+            V3 ud = unit_vector(rdir);
+            V3 refl = ud - 2 * dot(ud, nrm) * nrm;
+            ndir = refl + M.p[3] * random_in_unit_sphere(rng);
+            atten = v3(M.p[0], M.p[1], M.p[2]);
+          } else if (M.kind == MAT_DIELECTRIC) {  // material.h:285-324
+            float ri = M.p[0];
+            atten = v3(1.0f, 1.0f, 1.0f);
+            V3 reflected = rdir - 2 * dot(rdir, nrm) * nrm;
+            V3 outward;
+            float ni_over_nt, cosine;
+            if (dot(rdir, nrm) > 0) {
+              outward = -nrm;
+              ni_over_nt = ri;
+              cosine = dot(rdir, nrm) / length(rdir);
+            } else {
+              outward = nrm;
+              ni_over_nt = 1.0 / ri;
+              cosine = -dot(rdir, nrm) / length(rdir);
+            }
+            V3 uv = unit_vector(rdir);  // refract (material.h:21-32)
+            float dt = dot(uv, outward);
+            float disc = 1.0 - ni_over_nt * ni_over_nt * (1 - dt * dt);
+            float reflect_prob;
+            V3 refracted;
+            if (disc > 0) {
+              refracted = ni_over_nt * (uv - outward * dt) - outward * rsqrt_exact(disc);
+              float r0 = (1 - ri) / (1 + ri);  // schlick (material.h:14-19), pow(float,int) in double
+              r0 = r0 * r0;
+              reflect_prob = r0 + (1 - r0) * ::pow((double)(1 - cosine), 5.0);
+            } else {
+              reflect_prob = 1.0;
+            }
+            float r01 = drand(rng);
+            ndir = (r01 < reflect_prob) ? reflected : refracted;
+          } else {  // isotropic (material.h:362-367)
+            ndir = random_in_unit_sphere(rng);
+            atten = tex_value(S, M.tex, hu, hv, hpt);
+          }
+          P.rec_a[slot] = make_float4(atten.x, atten.y, atten.z, 0.f);
+          spec |= (1ull << depth);
+        } else {
+          // lambertian / orennayar / beckmann: mixture(light, bsdf) (Raytracing_n.cpp:73-94)
+          V3 atten = tex_value(S, M.tex, hu, hv, hpt);
+          Bsdf f;
+          f.kind = M.kind;
+          f.n = nrm;
+          f.uvw = onb_from_w(nrm);
+          f.A = M.p[0];
+          f.B = M.p[1];
+          f.dist.ax = M.p[0];
+          f.dist.ay = M.p[1];
+          f.beck_pdf = 0;
+          float pdf_val = 0;
+          if (S.n_lights > 0) {
+            (void)drand(rng);  // mixture_pdf ctor (pdf.h:175)
+            for (int guard = 0; pdf_val == 0 && guard < 100000; ++guard) {
+              if (drand(rng) < 0.5) ndir = lights_random(S, hpt, rng);
+              else ndir = bsdf_generate(f, rdir, rng);
+              pdf_val = 0.5 * lights_pdf(S, hpt, ndir) + 0.5 * bsdf_value(f, rdir, ndir);
+            }
+          } else {
+            ndir = bsdf_generate(f, rdir, rng);
+            pdf_val = bsdf_value(f, rdir, ndir);
+          }
+          float spdf = scattering_pdf(f, nrm, rdir, ndir);
+          V3 as = atten * spdf;
+          P.rec_a[slot] = make_float4(as.x, as.y, as.z, pdf_val);
+          P.rec_e[slot] = make_float4(emitted.x, emitted.y, emitted.z, 0.f);
+          ntime = ro.w;
+        }
+        P.ray_o[p] = make_float4(hpt.x, hpt.y, hpt.z, ntime);
+        P.ray_d[p] = make_float4(ndir.x, ndir.y, ndir.z, 0.f);
+        P.lcg[p] = rng.lcg;
+        P.pcg[p] = rng.pcg;
+        P.depth[p] = depth + 1;
+        P.spec[p] = spec;
+        alive = true;
+      } else {
+        finish_path(P, p, emitted, depth, spec, max_depth);  // return emitted (:97-100)
+      }
+    }
+  }
+  append(alive, p, next, next_count);
+}
+
+// acc[pixel] += samples in sample order (Raytracing_n.cpp:841), batch by batch
+__global__ void __launch_bounds__(256) k_accumulate(PathState P, BatchInfo B, float* acc) {
+  int lp = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lp >= B.n_paths / B.spp_batch) return;
+  size_t a = 3 * (size_t)(B.p0 + lp);
+  float cx = acc[a], cy = acc[a + 1], cz = acc[a + 2];
+  for (int s = 0; s < B.spp_batch; ++s) {
+    size_t q = 3 * ((size_t)lp * B.spp_batch + s);
+    cx += P.sample[q];
+    cy += P.sample[q + 1];
+    cz += P.sample[q + 2];
+  }
+  acc[a] = cx;
+  acc[a + 1] = cy;
+  acc[a + 2] = cz;
+}
+
+// col /= float(ns): k = 1.0 / t in double, stored to float (vec3.h:160-167)
+__global__ void k_finish(const float* acc, float* mean, int64_t n, int ns) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 3 * n) return;
+  float k = 1.0 / (float)ns;
+  mean[i] = acc[i] * k;
+}
+
+}  // namespace dev
+
+// ------------------------------------------------------------ launch shims
+void launch_raygen(const SceneView& S, const PathState& P, const BatchInfo& B, hipStream_t st) {
+  int g = (B.n_paths + 255) / 256;
+  hipLaunchKernelGGL(dev::k_raygen, dim3(g), dim3(256), 0, st, S, P, B);
+}
+void launch_trace(const SceneView& S, const PathState& P, const int* active, const int* count, int max_n,
+                  uint32_t* ctr, hipStream_t st) {
+  int g = (max_n + 255) / 256;
+  hipLaunchKernelGGL(dev::k_trace, dim3(g), dim3(256), 0, st, S, P, active, count, ctr);
+}
+void launch_shade(const SceneView& S, const PathState& P, const int* active, const int* count, int* next,
+                  int* next_count, int max_n, int max_depth, hipStream_t st) {
+  int g = (max_n + 255) / 256;
+  hipLaunchKernelGGL(dev::k_shade, dim3(g), dim3(256), 0, st, S, P, active, count, next, next_count, max_depth);
+}
+void launch_accumulate(const PathState& P, const BatchInfo& B, float* acc, hipStream_t st) {
+  int np = B.n_paths / B.spp_batch;
+  int g = (np + 255) / 256;
+  hipLaunchKernelGGL(dev::k_accumulate, dim3(g), dim3(256), 0, st, P, B, acc);
+}
+void launch_finish(const float* acc, float* mean, int64_t n, int ns, hipStream_t st) {
+  int64_t g = (3 * n + 255) / 256;
+  hipLaunchKernelGGL(dev::k_finish, dim3((unsigned)g), dim3(256), 0, st, acc, mean, n, ns);
+}
+
+}  // namespace srr

@@ -1,0 +1,909 @@
+// Host scene store, reference-compatible BVH builder, teapot tessellator, scene
+// text parser and flattener.  Host arithmetic follows the reference's float /
+// double promotions exactly (x86-64 baseline, no FMA), so the derived values
+// the device reads (boxes, camera frame, rotation sin/cos, material constants)
+// are bit-identical to the reference's.
+#include "scene.h"
+
+#include <cfloat>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <sstream>
+
+namespace srr {
+
+static const double kPi = 3.14159265358979323846;  // mathf.h:10
+static const uint64_t kPostPerlinSeed = 24561125610955ULL;
+
+#include "../../include/srr/teapot_data.inc"
+
+Scene::Scene() : lcg(kPostPerlinSeed) {}
+
+double Scene::drand48() {  // mathf.h:14-19
+  lcg = (0x5DEECE66DULL * lcg + 0xB16ULL) & 0xFFFFFFFFFFFFULL;
+  unsigned x = (unsigned)(lcg >> 16);
+  return (double)x / 4294967296.0;
+}
+
+// ----------------------------------------------------------------- small math
+static inline float ffmin(float a, float b) { return a < b ? a : b; }  // aabb.h:7-8
+static inline float ffmax(float a, float b) { return a > b ? a : b; }
+static inline void cross3(const float* a, const float* b, float* o) {
+  o[0] = a[1] * b[2] - a[2] * b[1];
+  o[1] = a[2] * b[0] - a[0] * b[2];
+  o[2] = a[0] * b[1] - a[1] * b[0];
+}
+static inline float len3(const float* v) { return std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]); }
+static inline void unit3(const float* v, float* o) {  // vec3.h:169-172
+  float l = len3(v);
+  o[0] = v[0] / l;
+  o[1] = v[1] / l;
+  o[2] = v[2] / l;
+}
+static inline Box3 surrounding(const Box3& a, const Box3& b) {  // aabb.h:54-62
+  Box3 r;
+  for (int k = 0; k < 3; ++k) {
+    r.mn[k] = ffmin(a.mn[k], b.mn[k]);
+    r.mx[k] = ffmax(a.mx[k], b.mx[k]);
+  }
+  return r;
+}
+
+// --------------------------------------------------------------- constructors
+int Scene::add_tex(HTex t) {
+  tex.push_back(std::move(t));
+  return (int)tex.size() - 1;
+}
+int Scene::add_mat(HMat m) {
+  mat.push_back(m);
+  return (int)mat.size() - 1;
+}
+int Scene::add_obj(HObj o) {
+  obj.push_back(std::move(o));
+  return (int)obj.size() - 1;
+}
+
+// Derived constants exactly as the reference's constructors compute them.
+int Scene::material(MatKind k, int t, const float* prm) {
+  HMat m;
+  m.kind = k;
+  m.tex = t;
+  switch (k) {
+    case MAT_METAL:  // material.h:245: fuzz = f < 1 ? f : 1
+      m.p[0] = prm[0]; m.p[1] = prm[1]; m.p[2] = prm[2];
+      m.p[3] = (prm[3] < 1) ? prm[3] : 1;
+      break;
+    case MAT_DIELECTRIC:
+      m.p[0] = prm[0];
+      break;
+    case MAT_ORENNAYAR: {  // material.h:129-133
+      float sigma = prm[0];
+      sigma = sigma / 180 * kPi;
+      m.p[0] = 1 - 0.5 * sigma * sigma / (sigma * sigma + 0.33);
+      m.p[1] = 0.45 * sigma * sigma / (sigma * sigma + 0.09);
+      break;
+    }
+    case MAT_BECKMANN:  // material.h:153-157 via RoughnessToAlpha (microfacet_distribution.h:139-144)
+      for (int q = 0; q < 2; ++q) {
+        float r = std::fmax(prm[q], 1e-3f);
+        float x = std::log(r);
+        m.p[q] = 1.62162f + 0.819955f * x + 0.1734f * x * x + 0.0171201f * x * x * x + 0.000640711f * x * x * x * x;
+      }
+      break;
+    default:
+      break;
+  }
+  return add_mat(m);
+}
+
+int Scene::sphere(const float c[3], float r, int m) {
+  HObj o;
+  o.kind = H_SPHERE;
+  o.mat = m;
+  std::memcpy(o.f, c, 12);
+  o.f[3] = r;
+  return add_obj(o);
+}
+
+int Scene::moving_sphere(const float c0[3], const float c1[3], float t0, float t1, float r, int m) {
+  HObj o;
+  o.kind = H_MSPHERE;
+  o.mat = m;
+  std::memcpy(o.f, c0, 12);
+  std::memcpy(o.f + 3, c1, 12);
+  o.f[6] = t0;
+  o.f[7] = t1;
+  o.f[8] = r;
+  return add_obj(o);
+}
+
+int Scene::rect(HKind k, float a0, float a1, float b0, float b1, float kk, int m) {
+  HObj o;
+  o.kind = k;
+  o.mat = m;
+  o.f[0] = a0; o.f[1] = a1; o.f[2] = b0; o.f[3] = b1; o.f[4] = kk;
+  return add_obj(o);
+}
+
+int Scene::box(const float p0[3], const float p1[3], int m) {  // box.h:18-29
+  int f[6];
+  f[0] = rect(H_XY, p0[0], p1[0], p0[1], p1[1], p1[2], m);
+  f[1] = wrap(H_FLIP, rect(H_XY, p0[0], p1[0], p0[1], p1[1], p0[2], m), nullptr);
+  f[2] = rect(H_XZ, p0[0], p1[0], p0[2], p1[2], p1[1], m);
+  f[3] = wrap(H_FLIP, rect(H_XZ, p0[0], p1[0], p0[2], p1[2], p0[1], m), nullptr);
+  f[4] = rect(H_YZ, p0[1], p1[1], p0[2], p1[2], p1[0], m);
+  f[5] = wrap(H_FLIP, rect(H_YZ, p0[1], p1[1], p0[2], p1[2], p0[0], m), nullptr);
+  HObj o;
+  o.kind = H_BOX;
+  o.mat = m;
+  std::memcpy(o.f, p0, 12);
+  std::memcpy(o.f + 3, p1, 12);
+  o.kids.assign(f, f + 6);
+  return add_obj(o);
+}
+
+int Scene::triangle(const float p[9], int m, const float* uv9, const float* n9) {  // triangle.h:13-50
+  HTri t;
+  std::memcpy(t.p, p, 36);
+  float e1[3] = {p[3] - p[0], p[4] - p[1], p[5] - p[2]};
+  float e2[3] = {p[6] - p[0], p[7] - p[1], p[8] - p[2]};
+  float c[3], nn[3];
+  cross3(e1, e2, c);
+  unit3(c, nn);
+  if (n9) std::memcpy(t.n, n9, 36);
+  else for (int k = 0; k < 3; ++k) std::memcpy(t.n + 3 * k, nn, 12);  // SURVEY Q5 build definition
+  if (uv9) std::memcpy(t.uv, uv9, 36);
+  else std::memset(t.uv, 0, 36);
+  t.mat = m;
+  tris.push_back(t);
+  HObj o;
+  o.kind = H_TRI;
+  o.mat = m;
+  o.tri = (int)tris.size() - 1;
+  return add_obj(o);
+}
+
+int Scene::wrap(HKind k, int child, const float* f) {
+  HObj o;
+  o.kind = k;
+  o.child = child;
+  if (f) std::memcpy(o.f, f, 12);
+  return add_obj(o);
+}
+
+int Scene::rotate(HKind k, int child, float angle) {  // hitable.h:81-107, 151-178
+  HObj o;
+  o.kind = k;
+  o.child = child;
+  float radians = (kPi / 180.) * angle;
+  float s = std::sin(radians), c = std::cos(radians);
+  o.f[0] = s;
+  o.f[1] = c;
+  Box3 b{};
+  o.has_box = bbox(child, 0, 1, b);
+  float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  for (int i = 0; i < 2; i++)
+    for (int j = 0; j < 2; j++)
+      for (int kk = 0; kk < 2; kk++) {
+        float x = i * b.mx[0] + (1 - i) * b.mn[0];
+        float y = j * b.mx[1] + (1 - j) * b.mn[1];
+        float z = kk * b.mx[2] + (1 - kk) * b.mn[2];
+        float t[3];
+        if (k == H_ROTY) {
+          t[0] = c * x + s * z; t[1] = y; t[2] = -s * x + c * z;
+        } else {
+          t[0] = x; t[1] = c * y + s * z; t[2] = -s * y + c * z;
+        }
+        for (int q = 0; q < 3; q++) {
+          if (t[q] > mx[q]) mx[q] = t[q];
+          if (t[q] < mn[q]) mn[q] = t[q];
+        }
+      }
+  std::memcpy(o.box.mn, mn, 12);
+  std::memcpy(o.box.mx, mx, 12);
+  return add_obj(o);
+}
+
+int Scene::medium(int boundary, float density, int t) {
+  HObj o;
+  o.kind = H_MEDIUM;
+  o.child = boundary;
+  o.f[0] = density;
+  o.tex = t;
+  return add_obj(o);
+}
+
+int Scene::list(const int* kids, int n) {
+  HObj o;
+  o.kind = H_LIST;
+  o.kids.assign(kids, kids + n);
+  return add_obj(o);
+}
+
+// glibc 2.35 qsort on an array of pointers is msort_with_tmp (stdlib/msort.c):
+// top-down, n1 = n/2, and the merge takes the LEFT element when cmp <= 0.  With
+// the reference's comparators (bvh.h:21-55, never 0) that fixes the order of
+// equal keys, which fixes the BVH topology.
+template <class T, class Cmp>
+static void msort_rec(T* b, size_t n, T* tmp, Cmp cmp) {
+  if (n <= 1) return;
+  size_t n1 = n / 2, n2 = n - n1;
+  T* b1 = b;
+  T* b2 = b + n1;
+  msort_rec(b1, n1, tmp, cmp);
+  msort_rec(b2, n2, tmp, cmp);
+  T* t = tmp;
+  while (n1 > 0 && n2 > 0) {
+    if (cmp(*b1, *b2) <= 0) { *t++ = *b1++; --n1; }
+    else { *t++ = *b2++; --n2; }
+  }
+  if (n1 > 0) std::memcpy(t, b1, n1 * sizeof(T));
+  std::memcpy(b, tmp, (n - n2) * sizeof(T));
+}
+
+int Scene::bvh(const int* kids, int n, float t0, float t1) {  // bvh.h:96-119
+  HBvh B;
+  std::vector<int> l(kids, kids + n);
+  B.input = l;
+  std::vector<int> tmp(n);
+  // boxes at times (0, 0) for the comparator, (t0, t1) for the node boxes
+  std::map<int, Box3> box00, boxT;
+  for (int h : l) {
+    Box3 b{};
+    bbox(h, 0, 0, b);
+    box00[h] = b;
+    bbox(h, t0, t1, b);
+    boxT[h] = b;
+  }
+  std::function<int(int*, int)> build = [&](int* a, int m) -> int {
+    int axis = int(3 * drand48());
+    auto cmp = [&](int x, int y) { return (box00[x].mn[axis] - box00[y].mn[axis] < 0.0) ? -1 : 1; };
+    msort_rec(a, (size_t)m, tmp.data(), cmp);
+    int me = (int)B.nodes.size();
+    B.nodes.push_back(HBvh::Node{});
+    int L, R;
+    Box3 bl, br;
+    if (m <= 2) {
+      auto leaf = [&](int h) {
+        B.leaves.push_back(h);
+        return ~((int)B.leaves.size() - 1);
+      };
+      L = leaf(a[0]);
+      R = (m == 1) ? L : leaf(a[1]);
+      bl = boxT[a[0]];
+      br = boxT[a[m - 1]];
+    } else {
+      L = build(a, m / 2);
+      R = build(a + m / 2, m - m / 2);
+      bl = B.nodes[L].box;
+      br = B.nodes[R].box;
+    }
+    B.nodes[me].left = L;
+    B.nodes[me].right = R;
+    B.nodes[me].box = surrounding(bl, br);
+    return me;
+  };
+  if (n < 1) return -22;
+  build(l.data(), n);
+  B.box = B.nodes[0].box;
+  bvhs.push_back(std::move(B));
+  HObj o;
+  o.kind = H_BVH;
+  o.bvh = (int)bvhs.size() - 1;
+  return add_obj(o);
+}
+
+void teapot_triangles(float scale, int divs, std::vector<float>& out) {  // teapot.h:19-37, 76-166
+  auto bez = [](const float* p, const float& t, float* o) {
+    float b0 = (1 - t) * (1 - t) * (1 - t);
+    float b1 = 3 * t * (1 - t) * (1 - t);
+    float b2 = 3 * t * t * (1 - t);
+    float b3 = t * t * t;
+    for (int c = 0; c < 3; ++c) o[c] = p[c] * b0 + p[3 + c] * b1 + p[6 + c] * b2 + p[9 + c] * b3;
+  };
+  std::vector<float> P((size_t)(divs + 1) * (divs + 1) * 3);
+  out.clear();
+  out.reserve((size_t)kSrrTeapotPatchCount * divs * divs * 2 * 9);
+  float cp[48];
+  for (int np = 0; np < kSrrTeapotPatchCount; ++np) {
+    for (int i = 0; i < 16; ++i)
+      for (int c = 0; c < 3; ++c) cp[i * 3 + c] = kSrrTeapotVertex[kSrrTeapotPatch[np * 16 + i] * 3 + c] * scale;
+    for (int j = 0, k = 0; j <= divs; ++j) {
+      float v = (float)j / (float)divs;
+      for (int i = 0; i <= divs; ++i, ++k) {
+        float u = (float)i / (float)divs;
+        float uc[12];
+        for (int q = 0; q < 4; ++q) bez(cp + 12 * q, u, uc + 3 * q);
+        bez(uc, v, &P[(size_t)k * 3]);
+      }
+    }
+    for (int j = 0; j < divs; ++j)
+      for (int i = 0; i < divs; ++i) {
+        int q[4] = {(divs + 1) * j + i, (divs + 1) * j + i + 1, (divs + 1) * (j + 1) + i + 1, (divs + 1) * (j + 1) + i};
+        for (int t = 0; t < 2; ++t)
+          for (int c : {q[0], q[t + 1], q[t + 2]})
+            for (int d = 0; d < 3; ++d) out.push_back(P[(size_t)c * 3 + d]);
+      }
+  }
+}
+
+int Scene::teapot(float scale, int divs, int m, int* first) {
+  std::vector<float> p;
+  teapot_triangles(scale, divs, p);
+  int n = (int)(p.size() / 9);
+  int f = -1;
+  for (int i = 0; i < n; ++i) {
+    int h = triangle(&p[(size_t)i * 9], m, nullptr, nullptr);
+    if (i == 0) f = h;
+  }
+  if (first) *first = f;
+  return n;
+}
+
+void Scene::camera(const float lf[3], const float la[3], const float vup[3], float vfov, float aspect,
+                   float aperture, float focus, float t0, float t1) {  // camera.h:33-48
+  HCamera& C = cam;
+  C.time0 = t0;
+  C.time1 = t1;
+  C.lens_radius = aperture / 2;
+  float theta = vfov * kPi / 180;
+  float half_height = std::tan(theta / 2);
+  float half_width = aspect * half_height;
+  std::memcpy(C.origin, lf, 12);
+  float d[3] = {lf[0] - la[0], lf[1] - la[1], lf[2] - la[2]};
+  float w[3], uu[3], vv[3], c[3];
+  unit3(d, w);
+  cross3(vup, w, c);
+  unit3(c, uu);
+  cross3(w, uu, vv);
+  for (int k = 0; k < 3; ++k) {
+    // origin - hw*focus*u - hh*focus*v - focus*w, evaluated left to right
+    float a = half_width * focus * uu[k];
+    float b = half_height * focus * vv[k];
+    float e = focus * w[k];
+    C.llc[k] = C.origin[k] - a - b - e;
+    C.horizontal[k] = 2 * half_width * focus * uu[k];
+    C.vertical[k] = 2 * half_height * focus * vv[k];
+    C.u[k] = uu[k];
+    C.v[k] = vv[k];
+  }
+  has_camera = true;
+}
+
+// ------------------------------------------------------------ bounding boxes
+bool Scene::bbox(int h, float t0, float t1, Box3& b) const {
+  const HObj& o = obj[h];
+  switch (o.kind) {
+    case H_SPHERE:  // sphere.h:31-34
+      for (int k = 0; k < 3; ++k) { b.mn[k] = o.f[k] - o.f[3]; b.mx[k] = o.f[k] + o.f[3]; }
+      return true;
+    case H_MSPHERE: {  // moving_sphere.h:19-21, 53-59
+      auto center = [&](float tm, float* c) {
+        float s = (tm - o.f[6]) / (o.f[7] - o.f[6]);
+        for (int k = 0; k < 3; ++k) c[k] = o.f[k] + s * (o.f[3 + k] - o.f[k]);
+      };
+      float c0[3], c1[3];
+      center(t0, c0);
+      center(t1, c1);
+      Box3 a, bb;
+      for (int k = 0; k < 3; ++k) {
+        a.mn[k] = c0[k] - o.f[8]; a.mx[k] = c0[k] + o.f[8];
+        bb.mn[k] = c1[k] - o.f[8]; bb.mx[k] = c1[k] + o.f[8];
+      }
+      b = surrounding(a, bb);
+      return true;
+    }
+    case H_XY: case H_XZ: case H_YZ: {  // aarect.h:11-14, 41-44, 72-75
+      int kax = o.kind == H_XY ? 2 : (o.kind == H_XZ ? 1 : 0);
+      int a0 = o.kind == H_YZ ? 1 : 0;
+      int a1 = o.kind == H_XY ? 1 : 2;
+      b.mn[a0] = o.f[0]; b.mx[a0] = o.f[1];
+      b.mn[a1] = o.f[2]; b.mx[a1] = o.f[3];
+      b.mn[kax] = o.f[4] - 0.0001;
+      b.mx[kax] = o.f[4] + 0.0001;
+      return true;
+    }
+    case H_BOX:  // box.h:10-13
+      for (int k = 0; k < 3; ++k) { b.mn[k] = o.f[k]; b.mx[k] = o.f[3 + k]; }
+      return true;
+    case H_TRI: {  // triangle.h:53-68
+      const float* p = tris[o.tri].p;
+      for (int k = 0; k < 3; ++k) {
+        b.mn[k] = ffmin(ffmin(p[k], p[3 + k]), p[6 + k]);
+        b.mx[k] = ffmax(ffmax(p[k], p[3 + k]), p[6 + k]);
+      }
+      return true;
+    }
+    case H_FLIP:
+      return bbox(o.child, t0, t1, b);
+    case H_TRANSLATE:  // hitable.h:54-61 (degenerate (Max+off, Max+off))
+      if (bbox(o.child, t0, t1, b)) {
+        for (int k = 0; k < 3; ++k) b.mn[k] = b.mx[k] = b.mx[k] + o.f[k];
+        return true;
+      }
+      return false;
+    case H_ROTY: case H_ROTX:
+      b = o.box;
+      return o.has_box;
+    case H_MEDIUM:
+      return bbox(o.child, t0, t1, b);
+    case H_LIST: {  // hitable_list.h:35-52 (merges list[0] only)
+      if (o.kids.empty()) return false;
+      Box3 tb;
+      if (!bbox(o.kids[0], t0, t1, tb)) return false;
+      b = tb;
+      for (size_t i = 0; i < o.kids.size(); ++i) {
+        if (bbox(o.kids[0], t0, t1, tb)) b = surrounding(b, tb);
+        else return false;
+      }
+      return true;
+    }
+    case H_BVH:
+      b = bvhs[o.bvh].box;
+      return true;
+  }
+  return false;
+}
+
+// ---------------------------------------------------------------- utilities
+uint64_t path_seed(uint32_t x, uint32_t y, uint32_t s, uint64_t base) {
+  uint64_t h = 0xcbf29ce484222325ULL ^ base;
+  const uint32_t w[3] = {x, y, s};
+  for (int k = 0; k < 3; ++k)
+    for (int b = 0; b < 4; ++b) {
+      h ^= (w[k] >> (8 * b)) & 0xffu;
+      h *= 0x100000001b3ULL;
+    }
+  return h & 0xFFFFFFFFFFFFULL;
+}
+
+void sobol2(unsigned N, double* pts) {  // Raytracing_n.cpp:721-812, D = 2
+  unsigned L = (unsigned)std::ceil(std::log((double)N) / std::log(2.0));
+  std::vector<unsigned> C(N ? N : 1);
+  C[0] = 1;
+  for (unsigned i = 1; i + 1 <= N; i++) {
+    C[i] = 1;
+    unsigned v = i;
+    while (v & 1) { v >>= 1; C[i]++; }
+  }
+  // dimension 1: all m_i = 1; dimension 2: joe-kuo line "2 1 0 1" (s=1, a=0, m1=1)
+  std::vector<unsigned> V1(L + 1), V2(L + 1);
+  for (unsigned i = 1; i <= L; i++) V1[i] = 1u << (32 - i);
+  if (L >= 1) V2[1] = 1u << 31;
+  for (unsigned i = 2; i <= L; i++) V2[i] = V2[i - 1] ^ (V2[i - 1] >> 1);
+  if (N) { pts[0] = 0; pts[1] = 0; }
+  unsigned X1 = 0, X2 = 0;
+  for (unsigned i = 1; i + 1 <= N; i++) {
+    X1 ^= V1[C[i - 1]];
+    X2 ^= V2[C[i - 1]];
+    pts[2 * i] = (double)X1 / std::pow(2.0, 32);
+    pts[2 * i + 1] = (double)X2 / std::pow(2.0, 32);
+  }
+}
+
+static inline uint32_t hash32(uint32_t a) {
+  a ^= a >> 16; a *= 0x7feb352dU; a ^= a >> 15; a *= 0x846ca68bU; a ^= a >> 16;
+  return a;
+}
+
+std::vector<uint8_t> gen_image(int w, int h, uint32_t seed, int kind) {
+  std::vector<uint8_t> px((size_t)w * h * 3);
+  for (int y = 0; y < h; ++y)
+    for (int x = 0; x < w; ++x) {
+      uint32_t n = hash32(seed * 0x9E3779B9u ^ hash32((uint32_t)(y * w + x)));
+      int r, g, b;
+      if (kind == 0) {
+        int t = (y * 255) / (h > 1 ? h - 1 : 1);
+        r = 90 + (t * 120) / 255 + (int)(n & 15);
+        g = 140 + (t * 90) / 255 + (int)((n >> 4) & 15);
+        b = 235 - (t * 60) / 255 + (int)((n >> 8) & 15);
+      } else if (kind == 1) {
+        int band = ((x * 7 + (int)((n >> 3) & 7)) / 13) & 15;
+        r = 110 + band * 6 + (int)(n & 7);
+        g = 70 + band * 4 + (int)((n >> 5) & 7);
+        b = 40 + band * 2 + (int)((n >> 9) & 7);
+      } else {
+        int c = ((x >> 3) ^ (y >> 3)) & 1;
+        r = g = b = c ? 230 : 25;
+      }
+      uint8_t* p = &px[((size_t)y * w + x) * 3];
+      p[0] = (uint8_t)(r > 255 ? 255 : r);
+      p[1] = (uint8_t)(g > 255 ? 255 : g);
+      p[2] = (uint8_t)(b > 255 ? 255 : b);
+    }
+  return px;
+}
+
+// Perlin tables (perlin.h:67-97): the reference builds them in static
+// initialisers from the global LCG at seed 1; vec3 arguments evaluate right to
+// left under g++, so each ranvec draws z, y, x.
+static void perlin_tables(std::vector<float>& ranvec, std::vector<int32_t>& perm) {
+  uint64_t s = 1;
+  auto dr = [&]() {
+    s = (0x5DEECE66DULL * s + 0xB16ULL) & 0xFFFFFFFFFFFFULL;
+    return (double)(unsigned)(s >> 16) / 4294967296.0;
+  };
+  ranvec.resize(256 * 3);
+  for (int i = 0; i < 256; ++i) {
+    float z = -1 + 2 * dr();
+    float y = -1 + 2 * dr();
+    float x = -1 + 2 * dr();
+    float v[3] = {x, y, z}, u[3];
+    unit3(v, u);
+    std::memcpy(&ranvec[i * 3], u, 12);
+  }
+  perm.resize(3 * 256);
+  for (int t = 0; t < 3; ++t) {
+    int32_t* p = &perm[t * 256];
+    for (int i = 0; i < 256; ++i) p[i] = i;
+    for (int i = 255; i > 0; i--) {
+      int target = int(dr() * (i + 1));
+      std::swap(p[i], p[target]);
+    }
+  }
+}
+
+// ----------------------------------------------------------------- flattening
+namespace {
+struct Flattener {
+  const Scene& S;
+  Flat& F;
+  std::string& err;
+  std::map<int, int> mesh_of_bvh;
+  std::vector<DObj> world, bound;
+  std::map<int, int> rect_row, sphere_row;
+
+  int chain_push(const std::vector<DXform>& ch) {
+    int b = (int)F.xforms.size();
+    F.xforms.insert(F.xforms.end(), ch.begin(), ch.end());
+    return b;
+  }
+  int add_rect(int h) {
+    auto it = rect_row.find(h);
+    if (it != rect_row.end()) return it->second;
+    const HObj& o = S.obj[h];
+    DRect r{};
+    r.kax = o.kind == H_XY ? 2 : (o.kind == H_XZ ? 1 : 0);
+    r.a0 = o.kind == H_YZ ? 1 : 0;
+    r.a1 = o.kind == H_XY ? 1 : 2;
+    r.lo0 = o.f[0]; r.hi0 = o.f[1]; r.lo1 = o.f[2]; r.hi1 = o.f[3]; r.k = o.f[4];
+    r.mat = o.mat;
+    F.rects.push_back(r);
+    return rect_row[h] = (int)F.rects.size() - 1;
+  }
+  int add_sphere(int h) {
+    auto it = sphere_row.find(h);
+    if (it != sphere_row.end()) return it->second;
+    const HObj& o = S.obj[h];
+    DSphere s{};
+    if (o.kind == H_SPHERE) {
+      for (int k = 0; k < 3; ++k) s.c0[k] = s.c1[k] = o.f[k];
+      s.t0 = 0; s.t1 = 1; s.r = o.f[3];
+    } else {
+      for (int k = 0; k < 3; ++k) { s.c0[k] = o.f[k]; s.c1[k] = o.f[3 + k]; }
+      s.t0 = o.f[6]; s.t1 = o.f[7]; s.r = o.f[8];
+    }
+    s.mat = o.mat;
+    F.spheres.push_back(s);
+    return sphere_row[h] = (int)F.spheres.size() - 1;
+  }
+  int add_stri(int h) {
+    const HTri& t = S.tris[S.obj[h].tri];
+    DStandaloneTri d{};
+    std::memcpy(d.p, t.p, 36);
+    std::memcpy(d.sh.n, t.n, 36);
+    for (int k = 0; k < 3; ++k) { d.sh.uv[2 * k] = t.uv[3 * k]; d.sh.uv[2 * k + 1] = t.uv[3 * k + 1]; }
+    d.sh.mat = t.mat;
+    F.stris.push_back(d);
+    return (int)F.stris.size() - 1;
+  }
+  int add_mesh(int h) {  // a bvh_node whose leaves are all bare triangles
+    auto it = mesh_of_bvh.find(h);
+    if (it != mesh_of_bvh.end()) return it->second;
+    const HBvh& B = S.bvhs[S.obj[h].bvh];
+    for (int l : B.leaves)
+      if (S.obj[l].kind != H_TRI) return -1;
+    DMesh m{};
+    m.node_off = (int)(F.node_lo.size() / 4);
+    m.tri_off = (int)(F.tri_shade.size());
+    m.n_nodes = (int)B.nodes.size();
+    m.n_tris = (int)B.leaves.size();
+    for (const HBvh::Node& n : B.nodes) {
+      auto enc = [&](int c) -> int32_t { return c >= 0 ? c + m.node_off : ~(~c + m.tri_off); };
+      int32_t L = enc(n.left), R = enc(n.right);
+      float lf, rf;
+      std::memcpy(&lf, &L, 4);
+      std::memcpy(&rf, &R, 4);
+      F.node_lo.insert(F.node_lo.end(), {n.box.mn[0], n.box.mn[1], n.box.mn[2], lf});
+      F.node_hi.insert(F.node_hi.end(), {n.box.mx[0], n.box.mx[1], n.box.mx[2], rf});
+    }
+    for (int l : B.leaves) {
+      const HTri& t = S.tris[S.obj[l].tri];
+      for (int k = 0; k < 3; ++k) F.tri_pos.insert(F.tri_pos.end(), {t.p[3 * k], t.p[3 * k + 1], t.p[3 * k + 2], 0.f});
+      TriShade sh{};
+      std::memcpy(sh.n, t.n, 36);
+      for (int k = 0; k < 3; ++k) { sh.uv[2 * k] = t.uv[3 * k]; sh.uv[2 * k + 1] = t.uv[3 * k + 1]; }
+      sh.mat = t.mat;
+      F.tri_shade.push_back(sh);
+    }
+    F.meshes.push_back(m);
+    return mesh_of_bvh[h] = (int)F.meshes.size() - 1;
+  }
+
+  // Appends the objects `h` contributes to `out`, under transform chain `ch`.
+  bool walk(int h, std::vector<DXform> ch, std::vector<DObj>& out, bool in_medium) {
+    const HObj& o = S.obj[h];
+    auto emit = [&](int kind, int idx) {
+      DObj d;
+      d.kind = kind;
+      d.xf_begin = chain_push(ch);
+      d.xf_count = (int)ch.size();
+      d.idx = idx;
+      out.push_back(d);
+    };
+    switch (o.kind) {
+      case H_LIST:
+      case H_BOX:
+        // hitable_list::hit passes closest_so_far along in order, so a nested list
+        // (and box, box.h:31-33) behaves exactly like its children inlined in place.
+        for (int k : o.kids)
+          if (!walk(k, ch, out, in_medium)) return false;
+        return true;
+      case H_FLIP: ch.push_back(DXform{XF_FLIP, 0, 0, 0}); return walk(o.child, ch, out, in_medium);
+      case H_TRANSLATE: ch.push_back(DXform{XF_TRANSLATE, o.f[0], o.f[1], o.f[2]}); return walk(o.child, ch, out, in_medium);
+      case H_ROTY: ch.push_back(DXform{XF_ROTY, o.f[0], o.f[1], 0}); return walk(o.child, ch, out, in_medium);
+      case H_ROTX: ch.push_back(DXform{XF_ROTX, o.f[0], o.f[1], 0}); return walk(o.child, ch, out, in_medium);
+      case H_SPHERE:
+      case H_MSPHERE: emit(o.kind == H_SPHERE ? OBJ_SPHERE : OBJ_MSPHERE, add_sphere(h)); return true;
+      case H_XY: case H_XZ: case H_YZ: emit(OBJ_RECT, add_rect(h)); return true;
+      case H_TRI: emit(OBJ_TRI, add_stri(h)); return true;
+      case H_BVH: {
+        int m = add_mesh(h);
+        if (m < 0) {
+          err = "bvh_node over non-triangle hitables is not supported on the device yet";
+          return false;
+        }
+        emit(OBJ_MESH, m);
+        return true;
+      }
+      case H_MEDIUM: {
+        if (in_medium) {
+          err = "constant_medium nested inside a constant_medium boundary is not supported";
+          return false;
+        }
+        DMedium md{};
+        md.bnd_begin = (int)bound.size();
+        std::vector<DObj> tmp;
+        if (!walk(o.child, {}, tmp, true)) return false;
+        bound.insert(bound.end(), tmp.begin(), tmp.end());
+        md.bnd_count = (int)tmp.size();
+        md.density = o.f[0];
+        // constant_medium owns an isotropic phase material (constant_medium.h:6-9)
+        DMat iso{};
+        iso.kind = MAT_ISOTROPIC;
+        iso.tex = o.tex;
+        F.mats.push_back(iso);
+        md.phase_mat = (int)F.mats.size() - 1;
+        F.media.push_back(md);
+        emit(OBJ_MEDIUM, (int)F.media.size() - 1);
+        return true;
+      }
+    }
+    err = "unknown hitable";
+    return false;
+  }
+
+  DLight light(int h) {  // hitable_list.h:54-67 targets; flip forwards (aarect.h:163-169)
+    const HObj* o = &S.obj[h];
+    while (o->kind == H_FLIP) o = &S.obj[o->child];
+    int hh = (int)(o - S.obj.data());
+    if (o->kind == H_XZ) return DLight{LIGHT_XZRECT, add_rect(hh)};
+    if (o->kind == H_SPHERE) return DLight{LIGHT_SPHERE, add_sphere(hh)};
+    if (o->kind == H_TRI) return DLight{LIGHT_TRI, add_stri(hh)};
+    return DLight{LIGHT_NONE, 0};  // hitable defaults: pdf 0, random (1,0,0) (hitable.h:31-32)
+  }
+};
+}  // namespace
+
+int flatten(const Scene& S, Flat& F, std::string& err) {
+  F = Flat();
+  if (S.world < 0 || S.lights < 0 || !S.has_camera) {
+    err = "scene needs world, lights and a camera";
+    return -22;
+  }
+  if (S.obj[S.lights].kind != H_LIST) {
+    err = "lights must be a hitable_list (Raytracing_n.cpp:75 casts it)";
+    return -22;
+  }
+  // materials first: object rows reference them by handle
+  for (const HMat& m : S.mat) {
+    DMat d{};
+    d.kind = m.kind;
+    d.tex = m.tex;
+    std::memcpy(d.p, m.p, 16);
+    F.mats.push_back(d);
+  }
+  for (const HTex& t : S.tex) {
+    DTex d{};
+    d.kind = t.kind;
+    std::memcpy(d.c, t.c, 12);
+    d.nx = t.nx;
+    d.ny = t.ny;
+    d.even = t.even;
+    d.odd = t.odd;
+    if (t.kind == TEX_IMAGE) {
+      d.off = (int64_t)F.images.size();
+      F.images.insert(F.images.end(), t.px.begin(), t.px.end());
+    }
+    F.texs.push_back(d);
+  }
+  Flattener fl{S, F, err};
+  if (!fl.walk(S.world, {}, fl.world, false)) return -95;
+  F.n_world = (int)fl.world.size();
+  F.objs = fl.world;
+  for (DObj d : fl.bound) F.objs.push_back(d);
+  for (DMedium& m : F.media) m.bnd_begin += F.n_world;
+  for (int k : S.obj[S.lights].kids) {
+    if (S.obj[k].kind == H_LIST) {
+      err = "nested hitable_list inside the light list is not supported";
+      return -95;
+    }
+    F.lights.push_back(fl.light(k));
+  }
+  perlin_tables(F.perlin_ranvec, F.perlin_perm);
+  const HCamera& c = S.cam;
+  std::memcpy(F.cam.origin, c.origin, 12);
+  std::memcpy(F.cam.llc, c.llc, 12);
+  std::memcpy(F.cam.horizontal, c.horizontal, 12);
+  std::memcpy(F.cam.vertical, c.vertical, 12);
+  std::memcpy(F.cam.u, c.u, 12);
+  std::memcpy(F.cam.v, c.v, 12);
+  F.cam.time0 = c.time0;
+  F.cam.time1 = c.time1;
+  F.cam.lens_radius = c.lens_radius;
+  return 0;
+}
+
+// --------------------------------------------------------------- text parser
+namespace {
+struct Tok {
+  std::vector<std::string> t;
+  int line;
+  float f(size_t i) const { return std::strtof(t.at(i).c_str(), nullptr); }
+  long long i(size_t k) const { return std::strtoll(t.at(k).c_str(), nullptr, 10); }
+  unsigned long long u(size_t k) const { return std::strtoull(t.at(k).c_str(), nullptr, 10); }
+  void v3(size_t k, float* o) const { o[0] = f(k); o[1] = f(k + 1); o[2] = f(k + 2); }
+};
+}  // namespace
+
+int scene_from_text(const std::string& text, Scene& S, std::string& err) {
+  std::istringstream is(text);
+  std::string line;
+  int ln = 0;
+  bool header = false;
+  std::map<long long, int> T, M, O;
+  std::map<long long, std::pair<int, int>> G;  // group: first handle, count
+  auto need = [&](std::map<long long, int>& mp, long long id, const char* what) -> int {
+    if (id == -1 && std::string(what) == "mat") return -1;
+    auto it = mp.find(id);
+    if (it == mp.end()) throw std::runtime_error(std::string("undefined ") + what + " " + std::to_string(id));
+    return it->second;
+  };
+  try {
+    while (std::getline(is, line)) {
+      ++ln;
+      size_t h = line.find('#');
+      if (h != std::string::npos) line.resize(h);
+      Tok c;
+      c.line = ln;
+      std::istringstream ls(line);
+      std::string w;
+      while (ls >> w) c.t.push_back(w);
+      if (c.t.empty()) continue;
+      const std::string& k = c.t[0];
+      if (!header) {
+        if (k != "srr_scene" || c.i(1) != 1) throw std::runtime_error("not an srr_scene v1 description");
+        header = true;
+        continue;
+      }
+      float a[3], b[3], cc[3];
+      if (k == "lcg") S.lcg = c.u(1) & 0xFFFFFFFFFFFFULL;
+      else if (k == "tex") {
+        const std::string& t = c.t.at(2);
+        HTex x;
+        if (t == "const") { x.kind = TEX_CONST; c.v3(3, x.c); }
+        else if (t == "image_gen") {
+          x.kind = TEX_IMAGE;
+          x.nx = (int)c.i(3);
+          x.ny = (int)c.i(4);
+          x.px = gen_image(x.nx, x.ny, (uint32_t)c.u(5), (int)c.i(6));
+        } else if (t == "checker") {
+          x.kind = TEX_CHECKER;
+          x.even = need(T, c.i(3), "tex");
+          x.odd = need(T, c.i(4), "tex");
+        } else if (t == "noise") { x.kind = TEX_NOISE; x.c[0] = c.f(3); }
+        else throw std::runtime_error("tex kind " + t);
+        T[c.i(1)] = S.add_tex(std::move(x));
+      } else if (k == "mat") {
+        const std::string& t = c.t.at(2);
+        float prm[4] = {0, 0, 0, 0};
+        int hm;
+        if (t == "metal") { c.v3(3, prm); prm[3] = c.f(6); hm = S.material(MAT_METAL, -1, prm); }
+        else if (t == "dielectric") { prm[0] = c.f(3); hm = S.material(MAT_DIELECTRIC, -1, prm); }
+        else {
+          int tx = need(T, c.i(3), "tex");
+          if (t == "lambertian") hm = S.material(MAT_LAMBERTIAN, tx, prm);
+          else if (t == "orennayar") { prm[0] = c.f(4); hm = S.material(MAT_ORENNAYAR, tx, prm); }
+          else if (t == "beckmann") { prm[0] = c.f(4); prm[1] = c.f(5); hm = S.material(MAT_BECKMANN, tx, prm); }
+          else if (t == "diffuse_light") hm = S.material(MAT_DIFFUSE_LIGHT, tx, prm);
+          else if (t == "isotropic") hm = S.material(MAT_ISOTROPIC, tx, prm);
+          else throw std::runtime_error("mat kind " + t);
+        }
+        M[c.i(1)] = hm;
+      } else if (k == "grp") {
+        if (c.t.at(2) != "teapot") throw std::runtime_error("grp kind");
+        int first = -1;
+        int n = S.teapot(c.f(3), (int)c.i(4), need(M, c.i(5), "mat"), &first);
+        G[c.i(1)] = {first, n};
+      } else if (k == "obj") {
+        const std::string& t = c.t.at(2);
+        int hnd = -1;
+        if (t == "sphere") { c.v3(3, a); hnd = S.sphere(a, c.f(6), need(M, c.i(7), "mat")); }
+        else if (t == "moving_sphere") {
+          c.v3(3, a); c.v3(6, b);
+          hnd = S.moving_sphere(a, b, c.f(9), c.f(10), c.f(11), need(M, c.i(12), "mat"));
+        } else if (t == "xy_rect" || t == "xz_rect" || t == "yz_rect") {
+          HKind kk = t == "xy_rect" ? H_XY : (t == "xz_rect" ? H_XZ : H_YZ);
+          hnd = S.rect(kk, c.f(3), c.f(4), c.f(5), c.f(6), c.f(7), need(M, c.i(8), "mat"));
+        } else if (t == "box") { c.v3(3, a); c.v3(6, b); hnd = S.box(a, b, need(M, c.i(9), "mat")); }
+        else if (t == "triangle" || t == "triangle_uv" || t == "triangle_uvn") {
+          float p[9], uv[9], n[9];
+          for (int q = 0; q < 9; ++q) p[q] = c.f(3 + q);
+          if (t != "triangle") for (int q = 0; q < 9; ++q) uv[q] = c.f(13 + q);
+          if (t == "triangle_uvn") for (int q = 0; q < 9; ++q) n[q] = c.f(22 + q);
+          hnd = S.triangle(p, need(M, c.i(12), "mat"), t != "triangle" ? uv : nullptr,
+                           t == "triangle_uvn" ? n : nullptr);
+        } else if (t == "flip") hnd = S.wrap(H_FLIP, need(O, c.i(3), "obj"), nullptr);
+        else if (t == "translate") { c.v3(4, a); hnd = S.wrap(H_TRANSLATE, need(O, c.i(3), "obj"), a); }
+        else if (t == "rotate_y") hnd = S.rotate(H_ROTY, need(O, c.i(3), "obj"), c.f(4));
+        else if (t == "rotate_x") hnd = S.rotate(H_ROTX, need(O, c.i(3), "obj"), c.f(4));
+        else if (t == "constant_medium") hnd = S.medium(need(O, c.i(3), "obj"), c.f(4), need(T, c.i(5), "tex"));
+        else if (t == "list" || t == "bvh") {
+          size_t base = t == "bvh" ? 5 : 3;
+          long long n = c.i(base);
+          std::vector<int> kids;
+          for (long long q = 0; q < n; ++q) kids.push_back(need(O, c.i(base + 1 + q), "obj"));
+          hnd = t == "bvh" ? S.bvh(kids.data(), (int)n, c.f(3), c.f(4)) : S.list(kids.data(), (int)n);
+        } else if (t == "bvh_group" || t == "list_group") {
+          auto it = G.find(c.i(t == "bvh_group" ? 5 : 3));
+          if (it == G.end()) throw std::runtime_error("undefined grp");
+          std::vector<int> kids(it->second.second);
+          for (int q = 0; q < it->second.second; ++q) kids[q] = it->second.first + q;
+          hnd = t == "bvh_group" ? S.bvh(kids.data(), (int)kids.size(), c.f(3), c.f(4))
+                                 : S.list(kids.data(), (int)kids.size());
+        } else throw std::runtime_error("obj kind " + t);
+        if (hnd < 0) throw std::runtime_error("constructor failed");
+        O[c.i(1)] = hnd;
+        S.text_ids.emplace_back(c.i(1), hnd);
+      } else if (k == "camera") {
+        c.v3(1, a); c.v3(4, b); c.v3(7, cc);
+        S.camera(a, b, cc, c.f(10), c.f(11), c.f(12), c.f(13), c.f(14), c.f(15));
+      } else if (k == "world") S.world = need(O, c.i(1), "obj");
+      else if (k == "lights") S.lights = need(O, c.i(1), "obj");
+      else throw std::runtime_error("unknown command " + k);
+    }
+  } catch (const std::exception& e) {
+    err = "scene line " + std::to_string(ln) + ": " + e.what();
+    return -22;
+  }
+  if (!header) {
+    err = "empty scene description";
+    return -22;
+  }
+  return 0;
+}
+
+}  // namespace srr

@@ -1,0 +1,155 @@
+"""ctypes binding of libsrr.so (include/srr_capi.h) -- the host-side mirror of
+the reference's render driver (``renderthread``/``main``,
+Raytracing_n.cpp:815-952) over the C-ABI.  The HIP path is the only path:
+if libsrr.so is missing or no GPU is visible, calls fail loudly."""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG, "libsrr.so")
+_LIB = None
+
+FLAG_SORT_MATERIALS = 1
+FLAG_KEEP_PATHS = 2
+
+
+class SrrError(RuntimeError):
+    pass
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("nx", ctypes.c_int), ("ny", ctypes.c_int), ("spp", ctypes.c_int), ("max_depth", ctypes.c_int),
+                ("tile", ctypes.c_int), ("shard_index", ctypes.c_int), ("shard_count", ctypes.c_int),
+                ("batch_paths", ctypes.c_int), ("base_seed", ctypes.c_uint64), ("flags", ctypes.c_int)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("world_rays", ctypes.c_int64), ("paths", ctypes.c_int64), ("trace_launches", ctypes.c_int64),
+                ("trace_ms", ctypes.c_double), ("shade_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
+                ("bounces", ctypes.c_int64)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise SrrError(f"{LIB_PATH} not built (run __graft_entry__.build() or make -C simple-raytracing-render_amd)")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, ip, cp = ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p
+        L.srr_last_error.restype = cp
+        L.srr_version.restype = cp
+        L.srr_scene_from_text.argtypes = [cp, ctypes.POINTER(vp)]
+        L.srr_scene_destroy.argtypes = [vp]
+        L.srr_renderer_create.argtypes = [vp, ip, ctypes.POINTER(vp)]
+        L.srr_renderer_destroy.argtypes = [vp]
+        L.srr_shard_pixels.restype = ctypes.c_int64
+        L.srr_shard_pixels.argtypes = [ctypes.POINTER(Params), vp]
+        L.srr_render_device.argtypes = [vp, ctypes.POINTER(Params), vp, ctypes.POINTER(Stats)]
+        L.srr_render.argtypes = [vp, ctypes.POINTER(Params), vp, vp, ctypes.POINTER(Stats)]
+        L.srr_copy_paths.argtypes = [vp, vp, vp]
+        L.srr_tonemap.argtypes = [vp, ctypes.c_int64, vp]
+        L.srr_write_ppm.argtypes = [cp, ip, ip, vp]
+        L.srr_sobol_points.argtypes = [ip, vp]
+        _LIB = L
+    return _LIB
+
+
+def _check(rc):
+    if rc < 0:
+        raise SrrError(f"srr error {rc}: {lib().srr_last_error().decode()}")
+    return rc
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+def make_params(nx, ny, spp, max_depth=50, shard=(0, 1), tile=32, batch_paths=0, base_seed=0, flags=0):
+    return Params(nx, ny, spp, max_depth, tile, shard[0], shard[1], batch_paths, base_seed, flags)
+
+
+def shard_pixels(p: Params) -> np.ndarray:
+    n = _check(lib().srr_shard_pixels(ctypes.byref(p), None))
+    out = np.zeros(n, np.int32)
+    lib().srr_shard_pixels(ctypes.byref(p), _ptr(out))
+    return out
+
+
+def sobol_points(n: int) -> np.ndarray:
+    out = np.zeros((n, 2), np.float64)
+    _check(lib().srr_sobol_points(n, _ptr(out)))
+    return out
+
+
+class Scene:
+    """A scene parsed from srr scene description v1 text."""
+
+    def __init__(self, text: str):
+        h = ctypes.c_void_p()
+        _check(lib().srr_scene_from_text(text.encode(), ctypes.byref(h)))
+        self.h = h
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().srr_scene_destroy(self.h)
+            self.h = None
+
+
+class Renderer:
+    """Flattened scene resident on HIP device `device` (srr_renderer_create)."""
+
+    def __init__(self, scene, device: int = 0):
+        if isinstance(scene, str):
+            scene = Scene(scene)
+        self.scene = scene
+        h = ctypes.c_void_p()
+        _check(lib().srr_renderer_create(scene.h, device, ctypes.byref(h)))
+        self.h = h
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().srr_renderer_destroy(self.h)
+            self.h = None
+
+    def render(self, nx, ny, spp, max_depth=50, keep_paths=False, **kw):
+        """Whole image (or shard); returns dict(mean[n,3], img8[n,3], stats,
+        paths[n,spp,3], rays[n,spp] when keep_paths)."""
+        flags = kw.pop("flags", 0) | (FLAG_KEEP_PATHS if keep_paths else 0)
+        p = make_params(nx, ny, spp, max_depth, flags=flags, **kw)
+        n = shard_pixels(p).size
+        mean = np.zeros((n, 3), np.float32)
+        img8 = np.zeros((n, 3), np.uint8)
+        st = Stats()
+        _check(lib().srr_render(self.h, ctypes.byref(p), _ptr(mean), _ptr(img8), ctypes.byref(st)))
+        out = dict(mean=mean, img8=img8, stats=st.as_dict())
+        if keep_paths:
+            paths = np.zeros((n, spp, 3), np.float32)
+            rays = np.zeros((n, spp), np.uint8)
+            _check(lib().srr_copy_paths(self.h, _ptr(paths), _ptr(rays)))
+            out.update(paths=paths, rays=rays)
+        return out
+
+    def render_device(self, params: Params, d_mean_ptr: int) -> dict:
+        """Render into a device buffer (e.g. a torch tensor's data_ptr())."""
+        st = Stats()
+        _check(lib().srr_render_device(self.h, ctypes.byref(params), ctypes.c_void_p(d_mean_ptr), ctypes.byref(st)))
+        return st.as_dict()
+
+
+def tonemap(mean: np.ndarray) -> np.ndarray:
+    mean = np.ascontiguousarray(mean, np.float32)
+    out = np.zeros(mean.shape, np.uint8)
+    _check(lib().srr_tonemap(_ptr(mean), mean.size // 3, _ptr(out)))
+    return out
+
+
+def write_ppm(path: str, nx: int, ny: int, img8: np.ndarray) -> None:
+    img8 = np.ascontiguousarray(img8, np.uint8)
+    _check(lib().srr_write_ppm(path.encode(), nx, ny, _ptr(img8)))

@@ -1,0 +1,93 @@
+"""GPU parity: the HIP path, called through the C-ABI (libsrr.so), against
+(1) the REFERENCE's own per-path outputs (tests/golden/, made by
+oracle/ref from /root/reference), (2) the CPU restatement oracle at larger
+sizes, and (3) size-independent properties (shard / batch invariance).
+Tolerances: tests/parity.py."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle_bind as ob
+import parity
+from srr import capi, scenes
+
+pytestmark = pytest.mark.gpu
+META = json.load(open(os.path.join(ob.GOLDEN, "golden.json")))["renders"]
+
+
+def golden(name):
+    m = META[name]
+    n = m["nx"] * m["ny"]
+    text = open(os.path.join(ob.GOLDEN, f"{name}.scene")).read()
+    paths = np.fromfile(os.path.join(ob.GOLDEN, f"{name}.paths.f32"), np.float32).reshape(n, m["spp"], 3)
+    rays = np.fromfile(os.path.join(ob.GOLDEN, f"{name}.rays.u8"), np.uint8).reshape(n, m["spp"])
+    img = np.fromfile(os.path.join(ob.GOLDEN, f"{name}.img.f32"), np.float32).reshape(n, 3)
+    return m, text, paths, rays, img
+
+
+@pytest.mark.parametrize("name", sorted(META))
+def test_paths_match_reference(name):
+    m, text, gp, gr, gi = golden(name)
+    out = capi.Renderer(text).render(m["nx"], m["ny"], m["spp"], m["max_depth"], keep_paths=True)
+    pc = parity.compare_paths(out["paths"], gp)
+    ic = parity.compare_images(out["mean"], gi)
+    rays_eq = float((out["rays"] == gr).mean())
+    print(f"{name}: {pc} rays_eq={rays_eq:.5f} world_rays={out['stats']['world_rays']} "
+          f"(ref {m['world_rays']}) img={ic}")
+    assert pc["match"] >= parity.MIN_MATCH, pc
+    assert rays_eq >= parity.MIN_MATCH
+    assert abs(out["stats"]["world_rays"] - m["world_rays"]) <= 0.01 * m["world_rays"]
+    assert ic["mean_rel"] <= 0.005, ic
+
+
+def test_shards_assemble_to_the_same_image():
+    """Tile sharding: per-path seeds do not depend on the shard,
+    so the assembled image is bitwise the single-renderer image."""
+    sc, _ = scenes.s2_cornell_teapot()
+    r = capi.Renderer(sc.text())
+    nx, ny, spp = 48, 40, 8
+    full = r.render(nx, ny, spp, 50)["mean"]
+    asm = np.zeros_like(full)
+    for k in range(3):
+        part = r.render(nx, ny, spp, 50, shard=(k, 3), tile=16)["mean"]
+        px = capi.shard_pixels(capi.make_params(nx, ny, spp, shard=(k, 3), tile=16))
+        asm[px] = part
+    np.testing.assert_array_equal(asm.view(np.uint32), full.view(np.uint32))
+
+
+def test_batch_size_does_not_change_the_image():
+    sc, _ = scenes.s3_cornell_teapot_microfacet()
+    r = capi.Renderer(sc.text())
+    a = r.render(40, 40, 12, 50)["mean"]
+    b = r.render(40, 40, 12, 50, batch_paths=997)["mean"]  # ragged batches: pixel and sample splits
+    np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+@pytest.mark.parametrize("factory,nx,ny,spp", [
+    (scenes.s2_cornell_teapot, 256, 256, 16),
+    (lambda: scenes.s3_cornell_teapot_microfacet("beckmann"), 256, 256, 16),
+    (lambda: scenes.s4_soldier_standin(divs=20, fog=True), 192, 108, 8),
+])
+def test_larger_renders_match_oracle_on_sampled_pixels(factory, nx, ny, spp):
+    sc, _ = factory()
+    text = sc.text()
+    out = capi.Renderer(text).render(nx, ny, spp, 50, keep_paths=True)
+    rng = np.random.default_rng(7)
+    pix = np.sort(rng.choice(nx * ny, size=300, replace=False)).astype(np.int32)
+    ref = ob.render(text, nx, ny, spp, 50, pixels=pix, threads=8)
+    pc = parity.compare_paths(out["paths"][pix], ref["paths"])
+    print(pc)
+    assert pc["match"] >= parity.MIN_MATCH, pc
+
+
+def test_depth_limit_zero_and_one():
+    """maxDepth edge cases (Raytracing_n.cpp:63): depth 0 returns emitted only."""
+    sc, _ = scenes.s1_cornell()
+    text = sc.text()
+    for md in (0, 1):
+        out = capi.Renderer(text).render(16, 16, 4, md, keep_paths=True)
+        ref = ob.render(text, 16, 16, 4, md)
+        pc = parity.compare_paths(out["paths"], ref["paths"])
+        assert pc["match"] >= parity.MIN_MATCH, (md, pc)
