@@ -104,9 +104,12 @@ struct Rng {
 thread_local Rng R;
 inline double drand48() { return R.drand(); }
 
-// Traversal counters (SURVEY §8(d) N_node / N_tri / N_prim), per thread.
+// Traversal counters (SURVEY §8(d) N_node / N_tri / N_prim), per thread; only
+// work done inside world->hit counts (light-pdf probes are excluded).
 struct Counters { long long world = 0, node = 0, tri = 0, prim = 0; };
 thread_local Counters C;
+thread_local bool in_world = false;
+#define COUNT(f) do { if (in_world) ++C.f; } while (0)
 
 // ----------------------------------------------------------------- common.h
 template <typename T, typename U, typename W>
@@ -379,7 +382,7 @@ struct Hit {  // hitable.h:17-25
 struct AABB {  // aabb.h:10-52
   V mn, mx;
   bool hit(const Ray& r, float tmin, float tmax) const {
-    ++C.node;
+    COUNT(node);
     for (int a = 0; a < 3; a++) {
       float invD = 1.0f / r.B[a];
       float t0 = (mn[a] - r.A[a]) * invD;
@@ -421,7 +424,7 @@ struct Sphere : Hitable {  // sphere.h:17-86
   const Material* mat;
   Sphere(V c, float r, const Material* m) : center(c), radius(r), mat(m) {}
   bool hit(const Ray& r, float tmin, float tmax, Hit& rec, bool) const override {
-    ++C.prim;
+    COUNT(prim);
     V oc = r.A - center;
     float a = dot(r.B, r.B);
     float b = dot(oc, r.B);
@@ -476,7 +479,7 @@ struct MovingSphere : Hitable {  // moving_sphere.h:4-59
   const Material* mat;
   V center(float time) const { return c0 + ((time - t0) / (t1 - t0)) * (c1 - c0); }
   bool hit(const Ray& r, float tmin, float tmax, Hit& rec, bool) const override {
-    ++C.prim;
+    COUNT(prim);
     V oc = r.A - center(r.tm);
     float a = dot(r.B, r.B);
     float b = dot(oc, r.B);
@@ -512,7 +515,7 @@ struct Rect : Hitable {
   float lo0, hi0, lo1, hi1, k;
   const Material* mat;
   bool hit(const Ray& r, float tmin, float tmax, Hit& rec, bool) const override {  // aarect.h:96-147
-    ++C.prim;
+    COUNT(prim);
     float t = (k - r.A[kax]) / r.B[kax];
     if (t < tmin || t > tmax) return false;
     float x = r.A[a0] + t * r.B[a0];
@@ -701,7 +704,7 @@ struct Triangle : Hitable {  // triangle.h:9-188
   }
   // :117-188 -- ignores t0/t1 and returns t as a DISTANCE
   bool hit_side(bool front, const Ray& r, Hit& rec) const {
-    ++C.tri;
+    COUNT(tri);
     V e1 = p1 - p0, e2 = p2 - p0;
     if (!front) {
       e1 = p0 - p1;
@@ -1188,7 +1191,10 @@ struct Scene {
 V color(const Scene& S, const Ray& r, int* depth, int max_depth) {
   Hit h;
   ++C.world;
-  if (S.world->hit(r, 0.001, std::numeric_limits<float>::max(), h)) {
+  in_world = true;
+  bool hit_any = S.world->hit(r, 0.001, std::numeric_limits<float>::max(), h);
+  in_world = false;
+  if (hit_any) {
     Scatter s;
     V emitted = h.mat->emitted(r, h, h.u, h.v, h.p);
     float pdf_val = 0;

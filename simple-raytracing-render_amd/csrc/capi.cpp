@@ -12,8 +12,7 @@
 #include <vector>
 
 #include "../../include/srr_capi.h"
-#include "kernels.h"
-#include "scene.h"
+#include "renderer.h"
 
 using namespace srr;
 
@@ -43,84 +42,6 @@ int upload(T** dst, const std::vector<T>& v) {
   return 0;
 }
 }  // namespace
-
-struct srr_renderer {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  hipEvent_t ev[6] = {};  // trace beg/end, frame beg/end, shade beg/end
-  std::vector<void*> scene_bufs;
-  SceneView view{};
-  int n_objs = 0;
-  // path state (capacity cap paths x cap_depth records)
-  size_t cap = 0;
-  int cap_depth = 0;
-  PathState P{};
-  std::vector<void*> path_bufs;
-  int32_t* act[2] = {nullptr, nullptr};
-  int32_t* cnt = nullptr;  // 2 ints
-  uint32_t* ctr = nullptr; // 2 counters (box tests, triangle tests)
-  // frame buffers
-  float* acc = nullptr;
-  size_t acc_cap = 0;
-  int32_t* pixels = nullptr;
-  size_t pix_cap = 0;
-  double* sobol = nullptr;
-  int sobol_n = 0;
-  float* raw_all = nullptr;
-  uint8_t* rays_all = nullptr;
-  size_t keep_cap = 0;
-  int64_t kept_paths = 0;
-  uint64_t last_ctr[2] = {0, 0};
-
-  ~srr_renderer() {
-    if (device >= 0) hipSetDevice(device);
-    for (void* p : scene_bufs) hipFree(p);
-    free_paths();
-    hipFree(act[0]);
-    hipFree(act[1]);
-    hipFree(cnt);
-    hipFree(ctr);
-    hipFree(acc);
-    hipFree(pixels);
-    hipFree(sobol);
-    hipFree(raw_all);
-    hipFree(rays_all);
-    for (hipEvent_t e : ev)
-      if (e) hipEventDestroy(e);
-    if (stream) hipStreamDestroy(stream);
-  }
-  void free_paths() {
-    for (void* p : path_bufs) hipFree(p);
-    path_bufs.clear();
-    cap = 0;
-  }
-  template <class T>
-  int alloc(T** p, size_t n) {
-    HIPCHK(hipMalloc((void**)p, std::max<size_t>(n * sizeof(T), 16)));
-    path_bufs.push_back(*p);
-    return 0;
-  }
-  int ensure_paths(size_t n, int depth, bool keep) {
-    if (n <= cap && depth <= cap_depth && (!keep || P.raw)) return 0;
-    free_paths();
-    hipFree(act[0]);
-    hipFree(act[1]);
-    act[0] = act[1] = nullptr;
-    int d = std::max(depth, 1);
-    if (alloc(&P.ray_o, n) || alloc(&P.ray_d, n) || alloc(&P.lcg, n) || alloc(&P.pcg, n) || alloc(&P.depth, n) ||
-        alloc(&P.spec, n) || alloc(&P.hit_p, n) || alloc(&P.hit_n, n) || alloc(&P.hit_mat, n) ||
-        alloc(&P.rec_a, n * d) || alloc(&P.rec_e, n * d) || alloc(&P.sample, 3 * n))
-      return SRR_ENOMEM;
-    P.raw = nullptr;
-    P.rays = nullptr;
-    if (keep && (alloc(&P.raw, 3 * n) || alloc(&P.rays, n))) return SRR_ENOMEM;
-    HIPCHK(hipMalloc((void**)&act[0], n * sizeof(int32_t)));
-    HIPCHK(hipMalloc((void**)&act[1], n * sizeof(int32_t)));
-    cap = n;
-    cap_depth = d;
-    return 0;
-  }
-};
 
 extern "C" {
 
@@ -339,55 +260,9 @@ int srr_renderer_create(const srr_scene* sc, int device, srr_renderer** out) {
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
     return fail(SRR_ENODEV, "no HIP device (the srr renderer has no CPU fallback)");
   if (device < 0 || device >= ndev) return fail(SRR_ENODEV, "device index out of range");
-  Flat F;
   std::string err;
-  int rc = flatten(sc->s, F, err);
+  int rc = renderer_create(sc->s, device, out, err);
   if (rc < 0) return fail(rc, err);
-  std::unique_ptr<srr_renderer> r(new srr_renderer());
-  r->device = device;
-  HIPCHK(hipSetDevice(device));
-  HIPCHK(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking));
-  for (auto& e : r->ev) HIPCHK(hipEventCreate(&e));
-  auto up = [&](auto** dst, const auto& vec) -> int {
-    int q = upload(dst, vec);
-    if (q == 0) r->scene_bufs.push_back((void*)*dst);
-    return q;
-  };
-  DObj* objs; DXform* xf; DSphere* sph; DRect* rc_; DStandaloneTri* st; DMesh* me; float* nlo; float* nhi;
-  float* tp; TriShade* ts; DMedium* md; DMat* mt; DTex* tx; uint8_t* im; float* pr; int32_t* pp; DLight* li;
-  std::vector<DCamera> cam{F.cam};
-  DCamera* cm;
-  if (up(&objs, F.objs) || up(&xf, F.xforms) || up(&sph, F.spheres) || up(&rc_, F.rects) || up(&st, F.stris) ||
-      up(&me, F.meshes) || up(&nlo, F.node_lo) || up(&nhi, F.node_hi) || up(&tp, F.tri_pos) ||
-      up(&ts, F.tri_shade) || up(&md, F.media) || up(&mt, F.mats) || up(&tx, F.texs) || up(&im, F.images) ||
-      up(&pr, F.perlin_ranvec) || up(&pp, F.perlin_perm) || up(&li, F.lights) || up(&cm, cam))
-    return SRR_EIO;
-  SceneView& V = r->view;
-  V.objs = objs;
-  V.n_world = F.n_world;
-  V.has_media = F.media.empty() ? 0 : 1;
-  V.xforms = xf;
-  V.spheres = sph;
-  V.rects = rc_;
-  V.stris = st;
-  V.meshes = me;
-  V.node_lo = (const float4*)nlo;
-  V.node_hi = (const float4*)nhi;
-  V.tri_pos = (const float4*)tp;
-  V.tri_shade = ts;
-  V.media = md;
-  V.mats = mt;
-  V.texs = tx;
-  V.images = im;
-  V.perlin_ranvec = pr;
-  V.perlin_perm = pp;
-  V.lights = li;
-  V.n_lights = (int)F.lights.size();
-  V.cam = cm;
-  r->n_objs = (int)F.objs.size();
-  HIPCHK(hipMalloc((void**)&r->cnt, 4 * sizeof(int32_t)));
-  HIPCHK(hipMalloc((void**)&r->ctr, 4 * sizeof(uint32_t)));
-  *out = r.release();
   return 0;
 }
 
@@ -418,120 +293,13 @@ int64_t srr_shard_pixels(const srr_params* p, int32_t* out) {
 int srr_render_device(srr_renderer* r, const srr_params* p, float* d_mean, srr_stats* stats) {
   if (!r || !p || !d_mean) return fail(SRR_EINVAL, "null argument");
   if (p->spp < 1 || p->max_depth < 0 || p->max_depth > 64) return fail(SRR_EINVAL, "spp >= 1, 0 <= max_depth <= 64");
-  HIPCHK(hipSetDevice(r->device));
   int64_t npix = srr_shard_pixels(p, nullptr);
   if (npix < 0) return (int)npix;
   std::vector<int32_t> pix(npix);
   srr_shard_pixels(p, pix.data());
-  hipStream_t st = r->stream;
-  bool keep = (p->flags & SRR_FLAG_KEEP_PATHS) != 0;
-  // buffers
-  if ((size_t)npix > r->pix_cap) {
-    hipFree(r->pixels);
-    hipFree(r->acc);
-    HIPCHK(hipMalloc((void**)&r->pixels, npix * sizeof(int32_t)));
-    HIPCHK(hipMalloc((void**)&r->acc, 3 * npix * sizeof(float)));
-    r->pix_cap = npix;
-  }
-  HIPCHK(hipMemcpyAsync(r->pixels, pix.data(), npix * sizeof(int32_t), hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemsetAsync(r->acc, 0, 3 * npix * sizeof(float), st));
-  if (p->spp > r->sobol_n) {
-    hipFree(r->sobol);
-    HIPCHK(hipMalloc((void**)&r->sobol, 2 * p->spp * sizeof(double)));
-    r->sobol_n = p->spp;
-  }
-  std::vector<double> sp(2 * (size_t)p->spp);
-  sobol2((unsigned)p->spp, sp.data());
-  HIPCHK(hipMemcpyAsync(r->sobol, sp.data(), sp.size() * sizeof(double), hipMemcpyHostToDevice, st));
-  if (keep) {
-    size_t need = (size_t)npix * p->spp;
-    if (need > r->keep_cap) {
-      hipFree(r->raw_all);
-      hipFree(r->rays_all);
-      HIPCHK(hipMalloc((void**)&r->raw_all, need * 3 * sizeof(float)));
-      HIPCHK(hipMalloc((void**)&r->rays_all, need));
-      r->keep_cap = need;
-    }
-    r->kept_paths = (int64_t)need;
-  }
-  // batch geometry: pixels x samples per batch <= batch_paths
-  int64_t N = p->batch_paths > 0 ? p->batch_paths : (int64_t)1 << 21;
-  int64_t pix_chunk = std::min<int64_t>(npix, N);
-  int S = (int)std::max<int64_t>(1, std::min<int64_t>(p->spp, N / pix_chunk));
-  size_t cap = (size_t)pix_chunk * S;
-  int rc = r->ensure_paths(cap, p->max_depth, keep);
-  if (rc < 0) return rc;
-  if (!keep) { r->P.raw = nullptr; r->P.rays = nullptr; }
-  HIPCHK(hipMemsetAsync(r->ctr, 0, 4 * sizeof(uint32_t), st));
-
-  srr_stats s{};
-  auto t_wall = std::chrono::steady_clock::now();
-  HIPCHK(hipEventRecord(r->ev[2], st));
-  double trace_ms = 0, shade_ms = 0;
-  for (int64_t p0 = 0; p0 < npix; p0 += pix_chunk) {
-    int np = (int)std::min<int64_t>(pix_chunk, npix - p0);
-    for (int s0 = 0; s0 < p->spp; s0 += S) {
-      int Sb = std::min(S, p->spp - s0);
-      BatchInfo B{};
-      B.pixels = r->pixels;
-      B.sobol = r->sobol;
-      B.p0 = (int)p0;
-      B.n_paths = np * Sb;
-      B.s0 = s0;
-      B.spp_batch = Sb;
-      B.nx = p->nx;
-      B.ny = p->ny;
-      B.base_seed = p->base_seed;
-      PathState P = r->P;
-      P.active = r->act[0];
-      launch_raygen(r->view, P, B, st);
-      int n = B.n_paths;
-      HIPCHK(hipMemcpyAsync(r->cnt, &n, sizeof(int), hipMemcpyHostToDevice, st));
-      int cur = 0;
-      for (int bounce = 0; bounce <= p->max_depth && n > 0; ++bounce) {
-        HIPCHK(hipEventRecord(r->ev[0], st));
-        launch_trace(r->view, P, r->act[cur], r->cnt + cur, n, nullptr, st);
-        HIPCHK(hipEventRecord(r->ev[1], st));
-        HIPCHK(hipMemsetAsync(r->cnt + (cur ^ 1), 0, sizeof(int), st));
-        HIPCHK(hipEventRecord(r->ev[4], st));
-        launch_shade(r->view, P, r->act[cur], r->cnt + cur, r->act[cur ^ 1], r->cnt + (cur ^ 1), n, p->max_depth, st);
-        HIPCHK(hipEventRecord(r->ev[5], st));
-        int nn = 0;
-        HIPCHK(hipMemcpyAsync(&nn, r->cnt + (cur ^ 1), sizeof(int), hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
-        float ms = 0;
-        HIPCHK(hipEventElapsedTime(&ms, r->ev[0], r->ev[1]));
-        trace_ms += ms;
-        HIPCHK(hipEventElapsedTime(&ms, r->ev[4], r->ev[5]));
-        shade_ms += ms;
-        s.world_rays += n;
-        s.trace_launches += 1;
-        s.bounces += 1;
-        n = nn;
-        cur ^= 1;
-      }
-      launch_accumulate(P, B, r->acc, st);
-      if (keep) {
-        // batch paths are [pixel][sample-in-batch]; the frame keeps [pixel][spp]
-        HIPCHK(hipMemcpy2DAsync(r->raw_all + 3 * ((size_t)p0 * p->spp + s0), 3 * sizeof(float) * p->spp, P.raw,
-                                3 * sizeof(float) * Sb, 3 * sizeof(float) * Sb, np, hipMemcpyDeviceToDevice, st));
-        HIPCHK(hipMemcpy2DAsync(r->rays_all + ((size_t)p0 * p->spp + s0), p->spp, P.rays, Sb, Sb, np,
-                                hipMemcpyDeviceToDevice, st));
-      }
-      s.paths += B.n_paths;
-    }
-  }
-  launch_finish(r->acc, d_mean, npix, p->spp, st);
-  HIPCHK(hipEventRecord(r->ev[3], st));
-  HIPCHK(hipStreamSynchronize(st));
-  HIPCHK(hipGetLastError());
-  float total = 0;
-  HIPCHK(hipEventElapsedTime(&total, r->ev[2], r->ev[3]));
-  s.total_ms = total;
-  s.trace_ms = trace_ms;
-  s.shade_ms = shade_ms;
-  (void)t_wall;
-  if (stats) *stats = s;
+  std::string err;
+  int rc = render_device(r, p, pix.data(), npix, d_mean, stats, err);
+  if (rc < 0) return fail(rc, err);
   return 0;
 }
 

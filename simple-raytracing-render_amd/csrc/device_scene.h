@@ -6,9 +6,11 @@
 //                                           inlined in order, instance wrappers
 //                                           distributed onto each child as a
 //                                           transform chain (xforms[])
-//   mesh BVH       float4 node_lo/hi[2*N]   reference-topology BVH2 (bvh.h:96-119):
-//                                           lo = (min.xyz, left), hi = (max.xyz, right);
-//                                           child >= 0 node, < 0 ~triangle
+//   mesh BVH       float4 node_lo/hi[N]     reference-topology BVH2 (bvh.h:96-119) in
+//                                           preorder, threaded for stackless traversal:
+//                                           lo = (min.xyz, skip), hi = (max.xyz, leaf)
+//                                           skip = next node once this subtree is done;
+//                                           leaf = (first_tri << 1) | (count - 1), or -1
 //   triangles      float4 tri_pos[3*T]      p0, p1, p2 in BVH leaf (DFS) order
 //                  TriShade tri_shade[T]    n0..n2, uv0..uv2, material
 //   materials/textures/images/lights/camera   small tables

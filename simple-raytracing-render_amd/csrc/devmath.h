@@ -31,6 +31,26 @@ SRR_D float rdiv(float a, float b) { return __fdiv_rn(a, b); }
 
 static constexpr double kPi = 3.14159265358979323846;  // mathf.h:10
 
+// Comparisons of a float against a double literal that is not a float (the
+// reference's `det < 0.0001`, `fabs(x) > 0.9`) as exact float comparisons:
+// for float f and such a double d, f < d  <=>  f < up(d) and f > d <=> f >= up(d),
+// where up(d) is the smallest float above d.
+static constexpr float kUp1em4 = 0x1.a36e3p-14f;  // smallest float > 1e-4 (double)
+static constexpr float kUp0p9 = 0x1.cccccep-1f;   // smallest float > 0.9 (double)
+
+// Load of read-only scene data at a wave-uniform index through the constant
+// address space, so the compiler can use scalar (SMEM) loads: the kernels
+// write other buffers, which otherwise stops it from proving these never change.
+template <class T>
+SRR_D T cload(const T* p, int i) {
+  T v;
+  auto src = (const __attribute__((address_space(4))) uint32_t*)(p + i);
+  uint32_t* dst = (uint32_t*)&v;
+#pragma unroll
+  for (int w = 0; w < (int)(sizeof(T) / 4); ++w) dst[w] = src[w];
+  return v;
+}
+
 // vec3.h: float x3 value type; every operator is the reference's per-component op
 struct V3 {
   float x, y, z;

@@ -45,14 +45,16 @@ struct PathState {
   float4* hit_n;    // normal.xyz, v
   int32_t* hit_mat; // material row, -1 null material, -2 miss
   float4* rec_a;    // [path][max_depth]: attenuation*scattering_pdf (or attenuation), pdf
-  float4* rec_e;    // [path][max_depth]: emitted
   float* sample;    // [path][3] de_nan'd radiance
   float* raw;       // [path][3] radiance before de_nan (optional)
   uint8_t* rays;    // [path] world rays traced (optional)
-  int32_t* active;  // initial active list
 };
 
 struct BatchInfo {
+  int32_t* active;        // active list the batch's paths are appended to
+  int32_t* count;         // device count of that list, set to act0 + n_paths
+  int act0;               // ... at this offset
+  int slot0;              // first path-state slot of the batch's region
   const int32_t* pixels;  // shard pixel list (PPM-order indices)
   const double* sobol;    // [spp][2]
   int p0;                 // first shard pixel of the batch
@@ -64,9 +66,10 @@ struct BatchInfo {
 
 void launch_raygen(const SceneView& S, const PathState& P, const BatchInfo& B, hipStream_t st);
 void launch_trace(const SceneView& S, const PathState& P, const int* active, const int* count, int max_n,
-                  uint32_t* ctr, hipStream_t st);
-void launch_shade(const SceneView& S, const PathState& P, const int* active, const int* count, int* next,
-                  int* next_count, int max_n, int max_depth, hipStream_t st);
+                  int* lists, int list_cap, int* fam_count, int max_depth, uint32_t* ctr, hipStream_t st);
+void launch_shade(const SceneView& S, const PathState& P, const int* lists, int list_cap, const int* fam_count,
+                  int* next, int* next_count, int* region_alive, int region_size, int max_n, int max_depth,
+                  hipStream_t st);
 void launch_accumulate(const PathState& P, const BatchInfo& B, float* acc, hipStream_t st);
 void launch_finish(const float* acc, float* mean, int64_t n, int ns, hipStream_t st);
 

@@ -13,7 +13,9 @@
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
+#include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 
 #include "device_scene.h"
 #include "devmath.h"
@@ -71,7 +73,7 @@ SRR_D bool tri_hit(V3 p0, V3 p1, V3 p2, bool front, V3 o, V3 dir, float& t, floa
   V3 T;
   if (det > 0) T = o - p0;
   else { T = p0 - o; det = -det; }
-  if (det < 0.0001) return false;
+  if (det < kUp1em4) return false;  // det < 0.0001 (double)
   float uu = dot(T, P);
   if (uu < 0.0f || uu > det) return false;
   V3 Q = cross(T, e1);
@@ -82,25 +84,28 @@ SRR_D bool tri_hit(V3 p0, V3 p1, V3 p2, bool front, V3 o, V3 dir, float& t, floa
   tt *= inv;
   uu *= inv;
   vv *= inv;
-  if (tt < 0.0001) return false;
+  if (tt < kUp1em4) return false;  // t < 0.0001 (double)
   t = tt; u = uu; v = vv;
   return true;
 }
 
-// aabb.h:33-49 with the per-axis reciprocal hoisted (same value each test)
+// aabb.h:33-49 with the per-axis reciprocal hoisted (same value each test).
+// Branchless: the reference returns false at the first axis with tmax <= tmin;
+// tmin only grows and tmax only shrinks over the axes (NaN slabs leave both
+// unchanged), so testing once after all three axes gives the same answer.
 SRR_D bool slab(float4 lo, float4 hi, V3 o, V3 inv, float tmin, float tmax) {
 #define SRR_AX(A)                                     \
   {                                                   \
     float t0 = (lo.A - o.A) * inv.A;                  \
     float t1 = (hi.A - o.A) * inv.A;                  \
-    if (inv.A < 0.0f) { float s_ = t0; t0 = t1; t1 = s_; } \
-    tmin = t0 > tmin ? t0 : tmin;                     \
-    tmax = t1 < tmax ? t1 : tmax;                     \
-    if (tmax <= tmin) return false;                   \
+    bool sw = inv.A < 0.0f;                           \
+    float n_ = sw ? t1 : t0, f_ = sw ? t0 : t1;       \
+    tmin = n_ > tmin ? n_ : tmin;                     \
+    tmax = f_ < tmax ? f_ : tmax;                     \
   }
   SRR_AX(x) SRR_AX(y) SRR_AX(z)
 #undef SRR_AX
-  return true;
+  return !(tmax <= tmin);
 }
 
 struct MeshHit {
@@ -111,51 +116,62 @@ struct MeshHit {
 // bvh.h:64-93 over the reference-topology BVH: a node is tested against the
 // incoming [tmin, tmax] (never shrunk: the reference tests both children with
 // the same t_max), and among the tested triangles that hit, the smallest t wins,
-// ties to the later DFS leaf (left.t < right.t ? left : right).  Iterative with a
-// short stack; `counters` (optional) tallies box / triangle tests.
+// ties to the later DFS leaf (left.t < right.t ? left : right).  The reference
+// visits nodes left-first and never reorders, so a threaded preorder layout
+// (device_scene.h) reproduces its visit set exactly with no stack: box hit ->
+// next node (the left child); box miss or leaf done -> the skip link.
+template <bool PREFETCH>
 SRR_D bool mesh_hit(const SceneView& S, const DMesh& m, const Ray& r, float tmin, float tmax, bool is_medium,
                     MeshHit& out, uint32_t* ctr) {
   V3 inv = v3(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
   V3 dir = r.d / length(r.d);
-  int stack[64];
-  int sp = 0;
   int node = m.node_off;
+  const int end = m.node_off + m.n_nodes;
   bool found = false;
   float best_t = 0;
   int best_i = -1;
   uint32_t nbox = 0, ntri = 0;
+  float4 lo = S.node_lo[node], hi = S.node_hi[node];
   for (;;) {
-    float4 lo = S.node_lo[node];
-    float4 hi = S.node_hi[node];
     ++nbox;
-    if (slab(lo, hi, r.o, inv, tmin, tmax)) {
-      int L = __float_as_int(lo.w), R = __float_as_int(hi.w);
-      if (L < 0) {
-        // leaf: both children are triangles (L == R for the n == 1 leaf)
-        for (int k = 0; k < 2; ++k) {
-          int ti = ~(k == 0 ? L : R);
-          if (k == 1 && R == L) break;
-          const float4* tp = S.tri_pos + 3 * (size_t)ti;
-          float4 a = tp[0], b = tp[1], c = tp[2];
-          V3 p0 = v3(a.x, a.y, a.z), p1 = v3(b.x, b.y, b.z), p2 = v3(c.x, c.y, c.z);
-          float t, u, v;
-          ++ntri;
-          bool h = tri_hit(p0, p1, p2, true, r.o, dir, t, u, v);
-          if (!h && is_medium) { ++ntri; h = tri_hit(p0, p1, p2, false, r.o, dir, t, u, v); }
-          if (h && (!found || t < best_t || (t == best_t && ti > best_i))) {
-            found = true;
-            best_t = t;
-            best_i = ti;
-          }
+    const int skip = __float_as_int(lo.w);
+    const int leaf = __float_as_int(hi.w);
+    // both possible successors are known before the box test: fetch them now so
+    // their latency overlaps this node's work (one-node lookahead)
+    float4 lo_c, hi_c, lo_s, hi_s;
+    if (PREFETCH) {
+      if (leaf < 0) { lo_c = S.node_lo[node + 1]; hi_c = S.node_hi[node + 1]; }
+      if (skip < end) { lo_s = S.node_lo[skip]; hi_s = S.node_hi[skip]; }
+    }
+    bool hit = slab(lo, hi, r.o, inv, tmin, tmax);
+    if (hit && leaf >= 0) {
+      int first = leaf >> 1, count = (leaf & 1) + 1;
+      ntri += 2;  // the reference tests a one-triangle leaf twice (bvh.h:104-105)
+      for (int ti = first; ti < first + count; ++ti) {
+        const float4* tp = S.tri_pos + 3 * (size_t)ti;
+        float4 a = tp[0], b = tp[1], c = tp[2];
+        V3 p0 = v3(a.x, a.y, a.z), p1 = v3(b.x, b.y, b.z), p2 = v3(c.x, c.y, c.z);
+        float t, u, v;
+        bool h = tri_hit(p0, p1, p2, true, r.o, dir, t, u, v);
+        if (!h && is_medium) { ++ntri; h = tri_hit(p0, p1, p2, false, r.o, dir, t, u, v); }
+        if (h && (!found || t < best_t || (t == best_t && ti > best_i))) {
+          found = true;
+          best_t = t;
+          best_i = ti;
         }
-      } else {
-        if (sp < 64) stack[sp++] = R;
-        node = L;
-        continue;
       }
     }
-    if (sp == 0) break;
-    node = stack[--sp];
+    const bool down = hit && leaf < 0;
+    const int next = down ? node + 1 : skip;
+    if (next >= end) break;
+    if (PREFETCH) {
+      lo = down ? lo_c : lo_s;
+      hi = down ? hi_c : hi_s;
+    } else {
+      lo = S.node_lo[next];
+      hi = S.node_hi[next];
+    }
+    node = next;
   }
   if (ctr) { atomicAdd(ctr, nbox); atomicAdd(ctr + 1, ntri); }
   out.t = best_t;
@@ -167,7 +183,7 @@ SRR_D bool mesh_hit(const SceneView& S, const DMesh& m, const Ray& r, float tmin
 // 180-188; flip leaves the ray alone)
 SRR_D Ray chain_in(const SceneView& S, const DObj& ob, Ray r) {
   for (int k = 0; k < ob.xf_count; ++k) {
-    DXform x = S.xforms[ob.xf_begin + k];
+    DXform x = cload(S.xforms, ob.xf_begin + k);
     if (x.kind == XF_TRANSLATE) r.o = r.o - v3(x.a, x.b, x.c);
     else if (x.kind == XF_ROTY || x.kind == XF_ROTX) {
       int ia = x.kind == XF_ROTY ? 0 : 1;
@@ -210,18 +226,19 @@ struct ObjHit {
 };
 
 // hit of one non-medium flattened object (in its local frame)
+template <bool PF>
 SRR_D bool basic_hit(const SceneView& S, const DObj& ob, const Ray& lr, float tmin, float tmax, bool is_medium,
                      ObjHit& h, uint32_t* ctr) {
   switch (ob.kind) {
     case OBJ_SPHERE:
     case OBJ_MSPHERE:
-      return sphere_hit(S.spheres[ob.idx], ob.kind == OBJ_MSPHERE, lr, tmin, tmax, h.t);
+      return sphere_hit(cload(S.spheres, ob.idx), ob.kind == OBJ_MSPHERE, lr, tmin, tmax, h.t);
     case OBJ_RECT: {
       float u, v;
-      return rect_hit(S.rects[ob.idx], lr, tmin, tmax, h.t, u, v);
+      return rect_hit(cload(S.rects, ob.idx), lr, tmin, tmax, h.t, u, v);
     }
     case OBJ_TRI: {
-      const DStandaloneTri& T = S.stris[ob.idx];
+      const DStandaloneTri T = cload(S.stris, ob.idx);
       V3 p0 = v3(T.p[0], T.p[1], T.p[2]), p1 = v3(T.p[3], T.p[4], T.p[5]), p2 = v3(T.p[6], T.p[7], T.p[8]);
       V3 dir = lr.d / length(lr.d);
       float u, v;
@@ -231,7 +248,7 @@ SRR_D bool basic_hit(const SceneView& S, const DObj& ob, const Ray& lr, float tm
     }
     case OBJ_MESH: {
       MeshHit mh;
-      if (!mesh_hit(S, S.meshes[ob.idx], lr, tmin, tmax, is_medium, mh, ctr)) return false;
+      if (!mesh_hit<PF>(S, cload(S.meshes, ob.idx), lr, tmin, tmax, is_medium, mh, ctr)) return false;
       h.t = mh.t;
       h.prim = mh.tri;
       return true;
@@ -242,14 +259,15 @@ SRR_D bool basic_hit(const SceneView& S, const DObj& ob, const Ray& lr, float tm
 
 // hitable_list::hit (hitable_list.h:21-33) over objects [b, b+n) -- used for a
 // medium's boundary (which sees is_medium = true)
+template <bool PF>
 SRR_D bool list_hit(const SceneView& S, int b, int n, const Ray& r, float tmin, float tmax, bool is_medium, float& t,
                     uint32_t* ctr) {
   bool any = false;
   float closest = tmax;
   for (int k = 0; k < n; ++k) {
-    const DObj& ob = S.objs[b + k];
+    const DObj ob = cload(S.objs, b + k);
     ObjHit h;
-    if (basic_hit(S, ob, chain_in(S, ob, r), tmin, closest, is_medium, h, ctr)) {
+    if (basic_hit<PF>(S, ob, chain_in(S, ob, r), tmin, closest, is_medium, h, ctr)) {
       any = true;
       closest = h.t;
       t = h.t;
@@ -259,12 +277,13 @@ SRR_D bool list_hit(const SceneView& S, int b, int n, const Ray& r, float tmin, 
 }
 
 // constant_medium.h:19-50 (two draws, one even on a miss)
+template <bool PF>
 SRR_D bool medium_hit(const SceneView& S, const DMedium& md, const Ray& r, float tmin, float tmax, Rng& rng,
                       float& t, uint32_t* ctr) {
   (void)(drand(rng) < 0.00001);
   float t1, t2;
-  if (list_hit(S, md.bnd_begin, md.bnd_count, r, -FLT_MAX, FLT_MAX, true, t1, ctr)) {
-    if (list_hit(S, md.bnd_begin, md.bnd_count, r, t1 + 0.0001, FLT_MAX, true, t2, ctr)) {
+  if (list_hit<PF>(S, md.bnd_begin, md.bnd_count, r, -FLT_MAX, FLT_MAX, true, t1, ctr)) {
+    if (list_hit<PF>(S, md.bnd_begin, md.bnd_count, r, t1 + 0.0001, FLT_MAX, true, t2, ctr)) {
       if (t1 < tmin) t1 = tmin;
       if (t2 > tmax) t2 = tmax;
       if (t1 >= t2) return false;
@@ -289,20 +308,21 @@ struct WorldHit {
   float t;
 };
 
+template <bool MEDIA, bool PF>
 SRR_D WorldHit world_hit(const SceneView& S, const Ray& r, Rng& rng, uint32_t* ctr) {
   WorldHit w{-1, -1, 0};
   float closest = FLT_MAX;  // numeric_limits<float>::max(), Raytracing_n.cpp:58
   const float tmin = 0.001f;
   for (int k = 0; k < S.n_world; ++k) {
-    const DObj& ob = S.objs[k];
+    const DObj ob = cload(S.objs, k);
     Ray lr = chain_in(S, ob, r);
     ObjHit h;
     bool hit;
-    if (ob.kind == OBJ_MEDIUM) {
-      hit = medium_hit(S, S.media[ob.idx], lr, tmin, closest, rng, h.t, ctr);
+    if (MEDIA && ob.kind == OBJ_MEDIUM) {
+      hit = medium_hit<PF>(S, cload(S.media, ob.idx), lr, tmin, closest, rng, h.t, ctr);
       h.prim = -1;
     } else {
-      hit = basic_hit(S, ob, lr, tmin, closest, false, h, ctr);
+      hit = basic_hit<PF>(S, ob, lr, tmin, closest, false, h, ctr);
     }
     if (hit) {
       closest = h.t;
@@ -404,7 +424,7 @@ SRR_D HitRec world_record(const SceneView& S, const Ray& r, const WorldHit& w) {
 }
 
 // ================================================================ shading
-SRR_D V3 tex_value(const SceneView& S, int ti, float u, float v, V3 p) {
+SRR_D V3 tex_value_slow(const SceneView& S, int ti, float u, float v, V3 p) {
   // checker_texture recursion (texture.h:13-19) unrolled to a few levels
   for (int guard = 0; guard < 8; ++guard) {
     const DTex& T = S.texs[ti];
@@ -457,13 +477,19 @@ SRR_D V3 tex_value(const SceneView& S, int ti, float u, float v, V3 p) {
   return v3(0.f);
 }
 
+SRR_D V3 tex_value(const SceneView& S, int ti, float u, float v, V3 p) {
+  const DTex& T = S.texs[ti];
+  if (T.kind == TEX_CONST) return v3(T.c[0], T.c[1], T.c[2]);
+  return tex_value_slow(S, ti, u, v, p);
+}
+
 struct Onb {  // onb.h:21-30
   V3 u, v, w;
 };
 SRR_D Onb onb_from_w(V3 n) {
   Onb o;
   o.w = unit_vector(n);
-  V3 a = (fabsf(o.w.x) > 0.9) ? v3(0, 1, 0) : v3(1, 0, 0);
+  V3 a = (fabsf(o.w.x) >= kUp0p9) ? v3(0, 1, 0) : v3(1, 0, 0);  // fabs(w.x) > 0.9 (double)
   o.v = unit_vector(cross(o.w, a));
   o.u = cross(o.w, o.v);
   return o;
@@ -626,6 +652,8 @@ SRR_D V3 random_in_unit_sphere(Rng& rng) {
 }
 
 // light list (hitable_pdf over a hitable_list, hitable_list.h:54-67)
+__device__ __noinline__ float light_pdf_other(const SceneView& S, const DLight& L, V3 o, V3 v);
+
 SRR_D float light_pdf_one(const SceneView& S, const DLight& L, V3 o, V3 v) {
   Ray r{o, v, 0.0f};
   if (L.kind == LIGHT_XZRECT) {  // aarect.h:45-55
@@ -639,6 +667,12 @@ SRR_D float light_pdf_one(const SceneView& S, const DLight& L, V3 o, V3 v) {
     }
     return 0;
   }
+  if (L.kind == LIGHT_NONE) return 0.0;
+  return light_pdf_other(S, L, o, v);
+}
+
+__device__ __noinline__ float light_pdf_other(const SceneView& S, const DLight& L, V3 o, V3 v) {
+  Ray r{o, v, 0.0f};
   if (L.kind == LIGHT_SPHERE) {  // sphere.h:69-78
     const DSphere& s = S.spheres[L.idx];
     float t;
@@ -683,6 +717,8 @@ SRR_D float lights_pdf(const SceneView& S, V3 o, V3 v) {
   return sum;
 }
 
+__device__ __noinline__ V3 light_random_other(const SceneView& S, const DLight& L, V3 o, Rng& rng);
+
 SRR_D V3 lights_random(const SceneView& S, V3 o, Rng& rng) {
   int index = int(drand(rng) * S.n_lights);
   const DLight& L = S.lights[index];
@@ -692,6 +728,11 @@ SRR_D V3 lights_random(const SceneView& S, V3 o, Rng& rng) {
     float x = q.lo0 + drand(rng) * (q.hi0 - q.lo0);
     return v3(x, q.k, z) - o;
   }
+  if (L.kind == LIGHT_NONE) return v3(1, 0, 0);
+  return light_random_other(S, L, o, rng);
+}
+
+__device__ __noinline__ V3 light_random_other(const SceneView& S, const DLight& L, V3 o, Rng& rng) {
   if (L.kind == LIGHT_SPHERE) {  // sphere.h:7-15, 80-86
     const DSphere& s = S.spheres[L.idx];
     V3 dirc = v3(s.c0[0], s.c0[1], s.c0[2]) - o;
@@ -730,8 +771,9 @@ SRR_D V3 to_local_unit(const Onb& b, V3 d) {
   return unit_vector(v3(dot(ud, b.u), dot(ud, b.v), dot(ud, b.w)));
 }
 
+template <bool BECK>
 SRR_D V3 bsdf_generate(Bsdf& f, V3 wo, Rng& rng) {
-  if (f.kind == MAT_BECKMANN) {  // pdf.h:136-152
+  if (BECK) {  // pdf.h:136-152
     float u1 = pcg_uniform(rng);
     float u2 = pcg_uniform(rng);
     V3 mwo = -wo;
@@ -750,8 +792,9 @@ SRR_D V3 bsdf_generate(Bsdf& f, V3 wo, Rng& rng) {
   return onb_local(f.uvw, g);
 }
 
+template <bool BECK>
 SRR_D float bsdf_value(const Bsdf& f, V3 wo, V3 wi) {
-  if (f.kind == MAT_BECKMANN) return f.beck_pdf;
+  if (BECK) return f.beck_pdf;
   if (f.kind == MAT_LAMBERTIAN) {  // pdf.h:33-46
     float co = dot(unit_vector(wo), f.n);
     float ci = dot(unit_vector(wi), f.n);
@@ -782,8 +825,9 @@ SRR_D float bsdf_value(const Bsdf& f, V3 wo, V3 wi) {
   return cosine * (f.A + f.B * maxCos * sinAlpha * tanBeta) / kPi;
 }
 
+template <bool BECK>
 SRR_D float scattering_pdf(const Bsdf& f, V3 n, V3 rin, V3 sc) {
-  if (f.kind == MAT_BECKMANN) {  // material.h:160-185
+  if (BECK) {  // material.h:160-185
     V3 wo = to_local_unit(f.uvw, -rin);
     V3 wi = to_local_unit(f.uvw, sc);
     V3 wh = unit_vector(wi + wo);
@@ -812,10 +856,12 @@ __device__ __forceinline__ void append(bool pred, int value, int* list, int* cou
 }
 
 __global__ void __launch_bounds__(256) k_raygen(SceneView S, PathState P, BatchInfo B) {
-  int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= B.n_paths) return;
-  int lp = p / B.spp_batch;
-  int s = B.s0 + p % B.spp_batch;
+  int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= B.n_paths) return;
+  int lp = q / B.spp_batch;
+  int s = B.s0 + q % B.spp_batch;
+  int p = B.slot0 + q;
+  if (q == 0) *B.count = B.act0 + B.n_paths;
   int pix = B.pixels[B.p0 + lp];
   int i = pix % B.nx;
   int j = B.ny - 1 - pix / B.nx;  // Raytracing_n.cpp:827-828 (SURVEY Q12 fix)
@@ -855,29 +901,49 @@ __global__ void __launch_bounds__(256) k_raygen(SceneView S, PathState P, BatchI
   P.pcg[p] = rng.pcg;
   P.depth[p] = 0;
   P.spec[p] = 0;
-  P.active[p] = p;
+  B.active[B.act0 + q] = p;
   if (P.rays) P.rays[p] = 0;
 }
 
+// Material families for the per-bounce sort: the trace kernel bins every ray
+// into one list per family so each shade kernel carries only its family's
+// code (and registers).  Only diffuse_light emits and it never scatters, so a
+// scattering bounce always has emitted == 0 (material.h:89-92).
+enum Family : int { FAM_TERM = 0, FAM_DIFF = 1, FAM_BECK = 2, FAM_SPEC = 3 };
+
+SRR_D int family_of(int mat, int kind, int depth, int max_depth) {
+  if (mat < 0 || kind == MAT_DIFFUSE_LIGHT || depth >= max_depth) return FAM_TERM;  // Raytracing_n.cpp:63
+  if (kind == MAT_LAMBERTIAN || kind == MAT_ORENNAYAR) return FAM_DIFF;
+  if (kind == MAT_BECKMANN) return FAM_BECK;
+  return FAM_SPEC;
+}
+
+template <bool MEDIA, bool PF>
 __global__ void __launch_bounds__(256) k_trace(SceneView S, PathState P, const int* active, const int* count,
+                                               int* lists, int list_cap, int* fam_count, int max_depth,
                                                uint32_t* ctr) {
   int q = blockIdx.x * blockDim.x + threadIdx.x;
   int n = *count;
-  if (q >= n) return;
-  int p = active[q];
-  float4 ro = P.ray_o[p], rdv = P.ray_d[p];
-  Ray r{v3(ro.x, ro.y, ro.z), v3(rdv.x, rdv.y, rdv.z), ro.w};
-  Rng rng{P.lcg[p], P.pcg[p]};
-  WorldHit w = world_hit(S, r, rng, ctr);
-  if (S.has_media) P.lcg[p] = rng.lcg;
-  if (w.obj < 0) {
-    P.hit_mat[p] = -2;
-    return;
+  int p = -1, fam = -1;
+  if (q < n) {
+    p = active[q];
+    float4 ro = P.ray_o[p], rdv = P.ray_d[p];
+    Ray r{v3(ro.x, ro.y, ro.z), v3(rdv.x, rdv.y, rdv.z), ro.w};
+    Rng rng{P.lcg[p], P.pcg[p]};
+    WorldHit w = world_hit<MEDIA, PF>(S, r, rng, ctr);
+    if (MEDIA) P.lcg[p] = rng.lcg;
+    if (w.obj < 0) {
+      P.hit_mat[p] = -2;
+      fam = FAM_TERM;
+    } else {
+      HitRec h = world_record(S, r, w);
+      P.hit_p[p] = make_float4(h.p.x, h.p.y, h.p.z, h.u);
+      P.hit_n[p] = make_float4(h.n.x, h.n.y, h.n.z, h.v);
+      P.hit_mat[p] = h.mat;
+      fam = family_of(h.mat, h.mat >= 0 ? S.mats[h.mat].kind : -1, P.depth[p], max_depth);
+    }
   }
-  HitRec h = world_record(S, r, w);
-  P.hit_p[p] = make_float4(h.p.x, h.p.y, h.p.z, h.u);
-  P.hit_n[p] = make_float4(h.n.x, h.n.y, h.n.z, h.v);
-  P.hit_mat[p] = h.mat;
+  for (int f = 0; f < 4; ++f) append(fam == f, p, lists + f * list_cap, fam_count + f);
 }
 
 // Folds the recorded bounces back to front exactly like the recursion returns
@@ -886,12 +952,8 @@ __device__ void finish_path(const PathState& P, int p, V3 C, int depth, uint64_t
   for (int k = depth - 1; k >= 0; --k) {
     float4 a = P.rec_a[(size_t)p * max_depth + k];
     V3 av = v3(a.x, a.y, a.z);
-    if ((spec >> k) & 1) {
-      C = av * C;
-    } else {
-      float4 e = P.rec_e[(size_t)p * max_depth + k];
-      C = v3(e.x, e.y, e.z) + (av * C) / a.w;
-    }
+    if ((spec >> k) & 1) C = av * C;
+    else C = v3(0.f) + (av * C) / a.w;  // emitted (== 0) + attenuation*pdf*color / pdf_val
   }
   if (P.raw) {
     P.raw[3 * (size_t)p] = C.x;
@@ -907,122 +969,150 @@ __device__ void finish_path(const PathState& P, int p, V3 C, int depth, uint64_t
   P.sample[3 * (size_t)p + 2] = C.z;
 }
 
-__global__ void __launch_bounds__(256) k_shade(SceneView S, PathState P, const int* active, const int* count,
-                                               int* next, int* next_count, int max_depth) {
-  int q = blockIdx.x * blockDim.x + threadIdx.x;
-  int n = *count;
-  bool alive = false;
-  int p = -1;
-  if (q < n) {
-    p = active[q];
-    float4 ro = P.ray_o[p], rdv = P.ray_d[p];
-    V3 rdir = v3(rdv.x, rdv.y, rdv.z);
-    int depth = P.depth[p];
-    uint64_t spec = P.spec[p];
-    if (P.rays) P.rays[p] += 1;
-    int mat = P.hit_mat[p];
-    if (mat < 0) {
-      // miss -> vec3(0.0) (:104); a null material* is UB in the reference: 0 here
-      finish_path(P, p, v3(0.f), depth, spec, max_depth);
-    } else {
+// One hit of family F (color(), Raytracing_n.cpp:55-106).  Returns true when the
+// path continues with a new ray.
+template <int F>
+SRR_D bool shade_one(const SceneView& S, const PathState& P, int p, int max_depth) {
+  float4 ro = P.ray_o[p], rdv = P.ray_d[p];
+  V3 rdir = v3(rdv.x, rdv.y, rdv.z);
+  int depth = P.depth[p];
+  uint64_t spec = P.spec[p];
+  if (P.rays) P.rays[p] += 1;
+  int mat = P.hit_mat[p];
+  if (F == FAM_TERM) {
+    // miss -> vec3(0.0) (:104); a null material* is UB in the reference: 0 here;
+    // no scatter (light) or depth limit -> emitted (:97-100, material.h:348-354)
+    V3 emitted = v3(0.f);
+    if (mat >= 0) {
+      const DMat& M = S.mats[mat];
       float4 hp = P.hit_p[p], hn = P.hit_n[p];
-      V3 hpt = v3(hp.x, hp.y, hp.z), nrm = v3(hn.x, hn.y, hn.z);
-      float hu = hp.w, hv = hn.w;
-      const DMat M = S.mats[mat];
-      V3 emitted = v3(0.f);
-      if (M.kind == MAT_DIFFUSE_LIGHT && dot(nrm, rdir) < 0.0)  // material.h:348-354
-        emitted = tex_value(S, M.tex, hu, hv, hpt);
-      if (depth < max_depth && M.kind != MAT_DIFFUSE_LIGHT) {
-        Rng rng{P.lcg[p], P.pcg[p]};
-        V3 ndir;
-        float ntime = 0.0f;  // ray(a, b) defaults time to 0 (ray.h:10) for specular rays
-        size_t slot = (size_t)p * max_depth + depth;
-        if (M.kind == MAT_METAL || M.kind == MAT_DIELECTRIC || M.kind == MAT_ISOTROPIC) {
-          V3 atten;
-          if (M.kind == MAT_METAL) {  // material.h:248-256
-            V3 ud = unit_vector(rdir);
-            V3 refl = ud - 2 * dot(ud, nrm) * nrm;
-            ndir = refl + M.p[3] * random_in_unit_sphere(rng);
-            atten = v3(M.p[0], M.p[1], M.p[2]);
-          } else if (M.kind == MAT_DIELECTRIC) {  // material.h:285-324
-            float ri = M.p[0];
-            atten = v3(1.0f, 1.0f, 1.0f);
-            V3 reflected = rdir - 2 * dot(rdir, nrm) * nrm;
-            V3 outward;
-            float ni_over_nt, cosine;
-            if (dot(rdir, nrm) > 0) {
-              outward = -nrm;
-              ni_over_nt = ri;
-              cosine = dot(rdir, nrm) / length(rdir);
-            } else {
-              outward = nrm;
-              ni_over_nt = 1.0 / ri;
-              cosine = -dot(rdir, nrm) / length(rdir);
-            }
-            V3 uv = unit_vector(rdir);  // refract (material.h:21-32)
-            float dt = dot(uv, outward);
-            float disc = 1.0 - ni_over_nt * ni_over_nt * (1 - dt * dt);
-            float reflect_prob;
-            V3 refracted;
-            if (disc > 0) {
-              refracted = ni_over_nt * (uv - outward * dt) - outward * rsqrt_exact(disc);
-              float r0 = (1 - ri) / (1 + ri);  // schlick (material.h:14-19), pow(float,int) in double
-              r0 = r0 * r0;
-              reflect_prob = r0 + (1 - r0) * ::pow((double)(1 - cosine), 5.0);
-            } else {
-              reflect_prob = 1.0;
-            }
-            float r01 = drand(rng);
-            ndir = (r01 < reflect_prob) ? reflected : refracted;
-          } else {  // isotropic (material.h:362-367)
-            ndir = random_in_unit_sphere(rng);
-            atten = tex_value(S, M.tex, hu, hv, hpt);
-          }
-          P.rec_a[slot] = make_float4(atten.x, atten.y, atten.z, 0.f);
-          spec |= (1ull << depth);
-        } else {
-          // lambertian / orennayar / beckmann: mixture(light, bsdf) (Raytracing_n.cpp:73-94)
-          V3 atten = tex_value(S, M.tex, hu, hv, hpt);
-          Bsdf f;
-          f.kind = M.kind;
-          f.n = nrm;
-          f.uvw = onb_from_w(nrm);
-          f.A = M.p[0];
-          f.B = M.p[1];
-          f.dist.ax = M.p[0];
-          f.dist.ay = M.p[1];
-          f.beck_pdf = 0;
-          float pdf_val = 0;
-          if (S.n_lights > 0) {
-            (void)drand(rng);  // mixture_pdf ctor (pdf.h:175)
-            for (int guard = 0; pdf_val == 0 && guard < 100000; ++guard) {
-              if (drand(rng) < 0.5) ndir = lights_random(S, hpt, rng);
-              else ndir = bsdf_generate(f, rdir, rng);
-              pdf_val = 0.5 * lights_pdf(S, hpt, ndir) + 0.5 * bsdf_value(f, rdir, ndir);
-            }
-          } else {
-            ndir = bsdf_generate(f, rdir, rng);
-            pdf_val = bsdf_value(f, rdir, ndir);
-          }
-          float spdf = scattering_pdf(f, nrm, rdir, ndir);
-          V3 as = atten * spdf;
-          P.rec_a[slot] = make_float4(as.x, as.y, as.z, pdf_val);
-          P.rec_e[slot] = make_float4(emitted.x, emitted.y, emitted.z, 0.f);
-          ntime = ro.w;
-        }
-        P.ray_o[p] = make_float4(hpt.x, hpt.y, hpt.z, ntime);
-        P.ray_d[p] = make_float4(ndir.x, ndir.y, ndir.z, 0.f);
-        P.lcg[p] = rng.lcg;
-        P.pcg[p] = rng.pcg;
-        P.depth[p] = depth + 1;
-        P.spec[p] = spec;
-        alive = true;
+      V3 nrm = v3(hn.x, hn.y, hn.z);
+      if (M.kind == MAT_DIFFUSE_LIGHT && dot(nrm, rdir) < 0.0)
+        emitted = tex_value(S, M.tex, hp.w, hn.w, v3(hp.x, hp.y, hp.z));
+    }
+    finish_path(P, p, emitted, depth, spec, max_depth);
+    return false;
+  }
+  float4 hp = P.hit_p[p], hn = P.hit_n[p];
+  V3 hpt = v3(hp.x, hp.y, hp.z), nrm = v3(hn.x, hn.y, hn.z);
+  float hu = hp.w, hv = hn.w;
+  const DMat M = S.mats[mat];
+  Rng rng{P.lcg[p], P.pcg[p]};
+  V3 ndir;
+  float ntime = 0.0f;  // ray(a, b) defaults time to 0 (ray.h:10) for specular rays
+  size_t slot = (size_t)p * max_depth + depth;
+  if (F == FAM_SPEC) {
+    V3 atten;
+    if (M.kind == MAT_METAL) {  // material.h:248-256
+      V3 ud = unit_vector(rdir);
+      V3 refl = ud - 2 * dot(ud, nrm) * nrm;
+      ndir = refl + M.p[3] * random_in_unit_sphere(rng);
+      atten = v3(M.p[0], M.p[1], M.p[2]);
+    } else if (M.kind == MAT_DIELECTRIC) {  // material.h:285-324
+      float ri = M.p[0];
+      atten = v3(1.0f, 1.0f, 1.0f);
+      V3 reflected = rdir - 2 * dot(rdir, nrm) * nrm;
+      V3 outward;
+      float ni_over_nt, cosine;
+      if (dot(rdir, nrm) > 0) {
+        outward = -nrm;
+        ni_over_nt = ri;
+        cosine = dot(rdir, nrm) / length(rdir);
       } else {
-        finish_path(P, p, emitted, depth, spec, max_depth);  // return emitted (:97-100)
+        outward = nrm;
+        ni_over_nt = 1.0 / ri;
+        cosine = -dot(rdir, nrm) / length(rdir);
       }
+      V3 uv = unit_vector(rdir);  // refract (material.h:21-32)
+      float dt = dot(uv, outward);
+      float disc = 1.0 - ni_over_nt * ni_over_nt * (1 - dt * dt);
+      float reflect_prob;
+      V3 refracted;
+      if (disc > 0) {
+        refracted = ni_over_nt * (uv - outward * dt) - outward * rsqrt_exact(disc);
+        float r0 = (1 - ri) / (1 + ri);  // schlick (material.h:14-19), pow(float,int) in double
+        r0 = r0 * r0;
+        reflect_prob = r0 + (1 - r0) * ::pow((double)(1 - cosine), 5.0);
+      } else {
+        reflect_prob = 1.0;
+      }
+      float r01 = drand(rng);
+      ndir = (r01 < reflect_prob) ? reflected : refracted;
+    } else {  // isotropic (material.h:362-367)
+      ndir = random_in_unit_sphere(rng);
+      atten = tex_value(S, M.tex, hu, hv, hpt);
+    }
+    P.rec_a[slot] = make_float4(atten.x, atten.y, atten.z, 0.f);
+    spec |= (1ull << depth);
+  } else {
+    // lambertian / orennayar / beckmann: mixture(light, bsdf) (Raytracing_n.cpp:73-94)
+    V3 atten = tex_value(S, M.tex, hu, hv, hpt);
+    Bsdf f;
+    f.kind = (F == FAM_BECK) ? (int)MAT_BECKMANN : M.kind;
+    f.n = nrm;
+    f.uvw = onb_from_w(nrm);
+    f.A = M.p[0];
+    f.B = M.p[1];
+    f.dist.ax = M.p[0];
+    f.dist.ay = M.p[1];
+    f.beck_pdf = 0;
+    float pdf_val = 0;
+    if (S.n_lights > 0) {
+      (void)drand(rng);  // mixture_pdf ctor (pdf.h:175)
+      for (int guard = 0; pdf_val == 0 && guard < 100000; ++guard) {
+        if (drand(rng) < 0.5) ndir = lights_random(S, hpt, rng);
+        else ndir = bsdf_generate<F == FAM_BECK>(f, rdir, rng);
+        pdf_val = 0.5 * lights_pdf(S, hpt, ndir) + 0.5 * bsdf_value<F == FAM_BECK>(f, rdir, ndir);
+      }
+    } else {
+      ndir = bsdf_generate<F == FAM_BECK>(f, rdir, rng);
+      pdf_val = bsdf_value<F == FAM_BECK>(f, rdir, ndir);
+    }
+    float spdf = scattering_pdf<F == FAM_BECK>(f, nrm, rdir, ndir);
+    V3 as = atten * spdf;
+    P.rec_a[slot] = make_float4(as.x, as.y, as.z, pdf_val);
+    ntime = ro.w;
+  }
+  P.ray_o[p] = make_float4(hpt.x, hpt.y, hpt.z, ntime);
+  P.ray_d[p] = make_float4(ndir.x, ndir.y, ndir.z, 0.f);
+  P.lcg[p] = rng.lcg;
+  P.pcg[p] = rng.pcg;
+  P.depth[p] = depth + 1;
+  P.spec[p] = spec;
+  return true;
+}
+
+constexpr int kMaxRegions = 8;
+
+// Grid-stride over family F's list (sized on the device: no host readback);
+// survivors are compacted into `next` with one atomic per wave.
+template <int F>
+__global__ void __launch_bounds__(256) k_shade(SceneView S, PathState P, const int* lists, int list_cap,
+                                               const int* fam_count, int* next, int* next_count, int* region_alive,
+                                               int region_size, int max_depth) {
+  __shared__ int hist[kMaxRegions];
+  if (threadIdx.x < kMaxRegions) hist[threadIdx.x] = 0;
+  __syncthreads();
+  const int* list = lists + (size_t)F * list_cap;
+  const int n = fam_count[F];
+  for (int base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+    int q = base + threadIdx.x;
+    bool alive = false;
+    int p = -1;
+    if (q < n) {
+      p = list[q];
+      alive = shade_one<F>(S, P, p, max_depth);
+    }
+    if (F != FAM_TERM) {
+      append(alive, p, next, next_count);
+      // survivors per batch region, so the host knows when a batch has drained
+      if (alive) atomicAdd(&hist[p / region_size], 1);
     }
   }
-  append(alive, p, next, next_count);
+  if (F != FAM_TERM) {
+    __syncthreads();
+    if (threadIdx.x < kMaxRegions && hist[threadIdx.x]) atomicAdd(&region_alive[threadIdx.x], hist[threadIdx.x]);
+  }
 }
 
 // acc[pixel] += samples in sample order (Raytracing_n.cpp:841), batch by batch
@@ -1032,7 +1122,7 @@ __global__ void __launch_bounds__(256) k_accumulate(PathState P, BatchInfo B, fl
   size_t a = 3 * (size_t)(B.p0 + lp);
   float cx = acc[a], cy = acc[a + 1], cz = acc[a + 2];
   for (int s = 0; s < B.spp_batch; ++s) {
-    size_t q = 3 * ((size_t)lp * B.spp_batch + s);
+    size_t q = 3 * ((size_t)B.slot0 + (size_t)lp * B.spp_batch + s);
     cx += P.sample[q];
     cy += P.sample[q + 1];
     cz += P.sample[q + 2];
@@ -1058,14 +1148,37 @@ void launch_raygen(const SceneView& S, const PathState& P, const BatchInfo& B, h
   hipLaunchKernelGGL(dev::k_raygen, dim3(g), dim3(256), 0, st, S, P, B);
 }
 void launch_trace(const SceneView& S, const PathState& P, const int* active, const int* count, int max_n,
-                  uint32_t* ctr, hipStream_t st) {
+                  int* lists, int list_cap, int* fam_count, int max_depth, uint32_t* ctr, hipStream_t st) {
   int g = (max_n + 255) / 256;
-  hipLaunchKernelGGL(dev::k_trace, dim3(g), dim3(256), 0, st, S, P, active, count, ctr);
+  static const bool pf = [] {
+    const char* e = getenv("SRR_TRACE_PREFETCH");
+    return !(e && e[0] == '0');
+  }();
+#define SRR_LAUNCH_TRACE(M, F)                                                                              \
+  hipLaunchKernelGGL((dev::k_trace<M, F>), dim3(g), dim3(256), 0, st, S, P, active, count, lists, list_cap, \
+                     fam_count, max_depth, ctr)
+  if (S.has_media) {
+    if (pf) SRR_LAUNCH_TRACE(true, true);
+    else SRR_LAUNCH_TRACE(true, false);
+  } else {
+    if (pf) SRR_LAUNCH_TRACE(false, true);
+    else SRR_LAUNCH_TRACE(false, false);
+  }
+#undef SRR_LAUNCH_TRACE
 }
-void launch_shade(const SceneView& S, const PathState& P, const int* active, const int* count, int* next,
-                  int* next_count, int max_n, int max_depth, hipStream_t st) {
-  int g = (max_n + 255) / 256;
-  hipLaunchKernelGGL(dev::k_shade, dim3(g), dim3(256), 0, st, S, P, active, count, next, next_count, max_depth);
+void launch_shade(const SceneView& S, const PathState& P, const int* lists, int list_cap, const int* fam_count,
+                  int* next, int* next_count, int* region_alive, int region_size, int max_n, int max_depth,
+                  hipStream_t st) {
+  // grid sized for the whole bounce; each family kernel strides over its own list
+  int g = std::min((max_n + 255) / 256, 2048);
+  hipLaunchKernelGGL(dev::k_shade<dev::FAM_DIFF>, dim3(g), dim3(256), 0, st, S, P, lists, list_cap, fam_count, next,
+                     next_count, region_alive, region_size, max_depth);
+  hipLaunchKernelGGL(dev::k_shade<dev::FAM_BECK>, dim3(g), dim3(256), 0, st, S, P, lists, list_cap, fam_count, next,
+                     next_count, region_alive, region_size, max_depth);
+  hipLaunchKernelGGL(dev::k_shade<dev::FAM_SPEC>, dim3(g), dim3(256), 0, st, S, P, lists, list_cap, fam_count, next,
+                     next_count, region_alive, region_size, max_depth);
+  hipLaunchKernelGGL(dev::k_shade<dev::FAM_TERM>, dim3(g), dim3(256), 0, st, S, P, lists, list_cap, fam_count, next,
+                     next_count, region_alive, region_size, max_depth);
 }
 void launch_accumulate(const PathState& P, const BatchInfo& B, float* acc, hipStream_t st) {
   int np = B.n_paths / B.spp_batch;

@@ -1,0 +1,385 @@
+// Renderer: scene upload and the multi-lane wavefront driver (renderer.h).
+#include "renderer.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <thread>
+
+namespace srr {
+
+#define RCHK(x)                                                        \
+  do {                                                                 \
+    hipError_t e_ = (x);                                               \
+    if (e_ != hipSuccess) {                                            \
+      err = std::string(#x) + ": " + hipGetErrorString(e_);            \
+      return SRR_EIO;                                                  \
+    }                                                                  \
+  } while (0)
+
+template <class T>
+static hipError_t upload(T** dst, const std::vector<T>& v, std::vector<void*>& keep) {
+  size_t bytes = std::max<size_t>(v.size() * sizeof(T), 16);
+  hipError_t e = hipMalloc((void**)dst, bytes);
+  if (e != hipSuccess) return e;
+  keep.push_back(*dst);
+  if (!v.empty()) e = hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
+  return e;
+}
+
+int renderer_create(const Scene& sc, int device, srr_renderer** out, std::string& err) {
+  Flat F;
+  int rc = flatten(sc, F, err);
+  if (rc < 0) return rc;
+  std::unique_ptr<srr_renderer> r(new srr_renderer());
+  r->device = device;
+  if (const char* e = getenv("SRR_LANES")) r->n_lanes = std::max(1, std::min(kMaxLanes, atoi(e)));
+  RCHK(hipSetDevice(device));
+  std::vector<void*>& K = r->scene_bufs;
+  DObj* objs; DXform* xf; DSphere* sph; DRect* rct; DStandaloneTri* st; DMesh* me; float* nlo; float* nhi;
+  float* tp; TriShade* ts; DMedium* md; DMat* mt; DTex* tx; uint8_t* im; float* pr; int32_t* pp; DLight* li;
+  DCamera* cm;
+  std::vector<DCamera> cam{F.cam};
+  RCHK(upload(&objs, F.objs, K));
+  RCHK(upload(&xf, F.xforms, K));
+  RCHK(upload(&sph, F.spheres, K));
+  RCHK(upload(&rct, F.rects, K));
+  RCHK(upload(&st, F.stris, K));
+  RCHK(upload(&me, F.meshes, K));
+  RCHK(upload(&nlo, F.node_lo, K));
+  RCHK(upload(&nhi, F.node_hi, K));
+  RCHK(upload(&tp, F.tri_pos, K));
+  RCHK(upload(&ts, F.tri_shade, K));
+  RCHK(upload(&md, F.media, K));
+  RCHK(upload(&mt, F.mats, K));
+  RCHK(upload(&tx, F.texs, K));
+  RCHK(upload(&im, F.images, K));
+  RCHK(upload(&pr, F.perlin_ranvec, K));
+  RCHK(upload(&pp, F.perlin_perm, K));
+  RCHK(upload(&li, F.lights, K));
+  RCHK(upload(&cm, cam, K));
+  SceneView& V = r->view;
+  V.objs = objs;
+  V.n_world = F.n_world;
+  V.has_media = F.media.empty() ? 0 : 1;
+  V.xforms = xf;
+  V.spheres = sph;
+  V.rects = rct;
+  V.stris = st;
+  V.meshes = me;
+  V.node_lo = (const float4*)nlo;
+  V.node_hi = (const float4*)nhi;
+  V.tri_pos = (const float4*)tp;
+  V.tri_shade = ts;
+  V.media = md;
+  V.mats = mt;
+  V.texs = tx;
+  V.images = im;
+  V.perlin_ranvec = pr;
+  V.perlin_perm = pp;
+  V.lights = li;
+  V.n_lights = (int)F.lights.size();
+  V.cam = cm;
+  RCHK(hipStreamCreateWithFlags(&r->acc_st, hipStreamNonBlocking));
+  RCHK(hipEventCreate(&r->ev_beg));
+  RCHK(hipEventCreate(&r->ev_end));
+  for (int l = 0; l < kMaxLanes; ++l) {
+    Lane& L = r->lanes[l];
+    RCHK(hipStreamCreateWithFlags(&L.st, hipStreamNonBlocking));
+    RCHK(hipEventCreate(&L.ev_t0));
+    RCHK(hipEventCreate(&L.ev_t1));
+    RCHK(hipEventCreate(&L.ev_s1));
+    RCHK(hipEventCreateWithFlags(&L.ev_rb, hipEventDisableTiming));
+    for (int k = 0; k < kRegionsPerLane; ++k) {
+      RCHK(hipEventCreateWithFlags(&L.done_ev[k], hipEventDisableTiming));
+      RCHK(hipEventCreateWithFlags(&L.acc_ev[k], hipEventDisableTiming));
+    }
+    RCHK(hipMalloc((void**)&L.cnt, 16 * sizeof(int32_t)));
+    RCHK(hipHostMalloc((void**)&L.rb, 16 * sizeof(int32_t)));
+  }
+  *out = r.release();
+  return 0;
+}
+
+static void free_lane_paths(Lane& L) {
+  for (void* p : L.bufs) (void)hipFree(p);
+  L.bufs.clear();
+  L.cap = 0;
+  L.P = PathState{};
+  L.act[0] = L.act[1] = nullptr;
+  L.lists = nullptr;
+}
+
+template <class T>
+static hipError_t lane_alloc(Lane& L, T** p, size_t n) {
+  hipError_t e = hipMalloc((void**)p, std::max<size_t>(n * sizeof(T), 16));
+  if (e == hipSuccess) L.bufs.push_back(*p);
+  return e;
+}
+
+static int ensure_lane(Lane& L, size_t n, int depth, bool keep, std::string& err) {
+  int d = std::max(depth, 1);
+  if (n <= L.cap && d <= L.cap_depth && (!keep || L.has_raw)) return 0;
+  free_lane_paths(L);
+  PathState& P = L.P;
+  RCHK(lane_alloc(L, &P.ray_o, n));
+  RCHK(lane_alloc(L, &P.ray_d, n));
+  RCHK(lane_alloc(L, &P.lcg, n));
+  RCHK(lane_alloc(L, &P.pcg, n));
+  RCHK(lane_alloc(L, &P.depth, n));
+  RCHK(lane_alloc(L, &P.spec, n));
+  RCHK(lane_alloc(L, &P.hit_p, n));
+  RCHK(lane_alloc(L, &P.hit_n, n));
+  RCHK(lane_alloc(L, &P.hit_mat, n));
+  RCHK(lane_alloc(L, &P.rec_a, n * d));
+  RCHK(lane_alloc(L, &P.sample, 3 * n));
+  RCHK(lane_alloc(L, &L.lists, 4 * n));
+  RCHK(lane_alloc(L, &L.act[0], n));
+  RCHK(lane_alloc(L, &L.act[1], n));
+  L.has_raw = keep;
+  if (keep) {
+    RCHK(lane_alloc(L, &P.raw, 3 * n));
+    RCHK(lane_alloc(L, &P.rays, n));
+  }
+  L.cap = n;
+  L.cap_depth = d;
+  return 0;
+}
+
+int render_device(srr_renderer* r, const srr_params* p, const int32_t* pix, int64_t npix, float* d_mean,
+                  srr_stats* stats, std::string& err) {
+  RCHK(hipSetDevice(r->device));
+  const bool keep = (p->flags & SRR_FLAG_KEEP_PATHS) != 0;
+  const int R = kRegionsPerLane;
+  hipStream_t ast = r->acc_st;
+  // frame buffers
+  if ((size_t)npix > r->pix_cap) {
+    (void)hipFree(r->pixels);
+    (void)hipFree(r->acc);
+    r->pixels = nullptr;
+    r->acc = nullptr;
+    RCHK(hipMalloc((void**)&r->pixels, npix * sizeof(int32_t)));
+    RCHK(hipMalloc((void**)&r->acc, 3 * npix * sizeof(float)));
+    r->pix_cap = npix;
+  }
+  RCHK(hipMemcpy(r->pixels, pix, npix * sizeof(int32_t), hipMemcpyHostToDevice));
+  if (p->spp > r->sobol_n) {
+    (void)hipFree(r->sobol);
+    RCHK(hipMalloc((void**)&r->sobol, 2 * (size_t)p->spp * sizeof(double)));
+    r->sobol_n = p->spp;
+  }
+  std::vector<double> sp(2 * (size_t)p->spp);
+  sobol2((unsigned)p->spp, sp.data());
+  RCHK(hipMemcpy(r->sobol, sp.data(), sp.size() * sizeof(double), hipMemcpyHostToDevice));
+  if (keep) {
+    size_t need = (size_t)npix * p->spp;
+    if (need > r->keep_cap) {
+      (void)hipFree(r->raw_all);
+      (void)hipFree(r->rays_all);
+      RCHK(hipMalloc((void**)&r->raw_all, need * 3 * sizeof(float)));
+      RCHK(hipMalloc((void**)&r->rays_all, need));
+      r->keep_cap = need;
+    }
+    r->kept_paths = (int64_t)need;
+  }
+  // Batches: (pixel chunk, sample chunk) in the order every pixel must see its
+  // samples accumulated.
+  int64_t N = p->batch_paths > 0 ? p->batch_paths : (int64_t)1 << 20;
+  int64_t pix_chunk = std::min<int64_t>(npix, N);
+  int S = (int)std::max<int64_t>(1, std::min<int64_t>(p->spp, N / pix_chunk));
+  const int64_t region = pix_chunk * S;
+  std::vector<BatchInfo> batches;
+  for (int64_t p0 = 0; p0 < npix; p0 += pix_chunk) {
+    int np = (int)std::min<int64_t>(pix_chunk, npix - p0);
+    for (int s0 = 0; s0 < p->spp; s0 += S) {
+      BatchInfo B{};
+      B.pixels = r->pixels;
+      B.sobol = r->sobol;
+      B.p0 = (int)p0;
+      B.spp_batch = std::min(S, p->spp - s0);
+      B.n_paths = np * B.spp_batch;
+      B.s0 = s0;
+      B.nx = p->nx;
+      B.ny = p->ny;
+      B.base_seed = p->base_seed;
+      batches.push_back(B);
+    }
+  }
+  const size_t nb = batches.size();
+  // lanes: enough paths in flight to fill the GPU, without idle lanes on small frames
+  int lanes = (int)std::min<size_t>(nb, (size_t)r->n_lanes);
+  lanes = std::max(1, lanes);
+  size_t cap = (size_t)region * R;
+  if (cap > (size_t)INT32_MAX / 4) {
+    err = "batch_paths too large";
+    return SRR_EINVAL;
+  }
+  for (int l = 0; l < lanes; ++l) {
+    int rc = ensure_lane(r->lanes[l], cap, p->max_depth, keep, err);
+    if (rc < 0) return rc;
+  }
+  RCHK(hipDeviceSynchronize());
+  RCHK(hipMemsetAsync(r->acc, 0, 3 * npix * sizeof(float), ast));
+  RCHK(hipEventRecord(r->ev_beg, ast));
+  for (int l = 0; l < lanes; ++l) {
+    Lane& L = r->lanes[l];
+    L.n = 0;
+    L.cur = 0;
+    L.pending = false;
+    L.trace_ms = L.shade_ms = 0;
+    for (int k = 0; k < R; ++k) {
+      L.reg_batch[k] = -1;
+      L.acc_pending[k] = false;
+    }
+    if (!keep) {
+      L.P.raw = nullptr;
+      L.P.rays = nullptr;
+    }
+    RCHK(hipStreamWaitEvent(L.st, r->ev_beg, 0));
+  }
+  std::vector<int> b_lane(nb, -1), b_reg(nb, -1);
+  std::vector<char> b_done(nb, 0);
+  srr_stats s{};
+  size_t next_batch = 0, acc_head = 0;
+  const int64_t target = std::max<int64_t>(region, (int64_t)3 << 20) / 2;  // paths in flight per lane
+
+  while (acc_head < nb) {
+    bool progress = false;
+    for (int l = 0; l < lanes; ++l) {
+      Lane& L = r->lanes[l];
+      if (L.pending) {
+        hipError_t q = hipEventQuery(L.ev_rb);
+        if (q == hipErrorNotReady) continue;
+        RCHK(q);
+        L.pending = false;
+        progress = true;
+        float ms = 0;
+        RCHK(hipEventElapsedTime(&ms, L.ev_t0, L.ev_t1));
+        L.trace_ms += ms;
+        RCHK(hipEventElapsedTime(&ms, L.ev_t1, L.ev_s1));
+        L.shade_ms += ms;
+        L.n = L.rb[R];
+        for (int k = 0; k < R; ++k)
+          if (L.reg_batch[k] >= 0 && !b_done[L.reg_batch[k]] && L.rb[k] == 0) {
+            b_done[L.reg_batch[k]] = 1;
+            RCHK(hipEventRecord(L.done_ev[k], L.st));
+          }
+      }
+      // refill free regions with new batches
+      while (next_batch < nb && L.n < target) {
+        int fr = -1;
+        for (int k = 0; k < R; ++k)
+          if (L.reg_batch[k] < 0) {
+            fr = k;
+            break;
+          }
+        if (fr < 0) break;
+        if (L.acc_pending[fr]) {  // the region's previous batch is still being accumulated
+          RCHK(hipStreamWaitEvent(L.st, L.acc_ev[fr], 0));
+          L.acc_pending[fr] = false;
+        }
+        BatchInfo& B = batches[next_batch];
+        B.active = L.act[L.cur];
+        B.act0 = L.n;
+        B.slot0 = (int)(fr * region);
+        B.count = L.cnt + L.cur;
+        launch_raygen(r->view, L.P, B, L.st);
+        L.n += B.n_paths;
+        L.reg_batch[fr] = (int)next_batch;
+        b_lane[next_batch] = l;
+        b_reg[next_batch] = fr;
+        s.paths += B.n_paths;
+        ++next_batch;
+        progress = true;
+      }
+      if (L.n > 0) {
+        int n = L.n, cur = L.cur;
+        int* alive = L.cnt + 2;
+        int* fam = alive + R;
+        RCHK(hipMemsetAsync(L.cnt + (cur ^ 1), 0, sizeof(int), L.st));
+        RCHK(hipMemsetAsync(alive, 0, (R + 4) * sizeof(int), L.st));
+        RCHK(hipEventRecord(L.ev_t0, L.st));
+        launch_trace(r->view, L.P, L.act[cur], L.cnt + cur, n, L.lists, (int)L.cap, fam, p->max_depth, nullptr,
+                     L.st);
+        RCHK(hipEventRecord(L.ev_t1, L.st));
+        launch_shade(r->view, L.P, L.lists, (int)L.cap, fam, L.act[cur ^ 1], L.cnt + (cur ^ 1), alive, (int)region,
+                     n, p->max_depth, L.st);
+        RCHK(hipEventRecord(L.ev_s1, L.st));
+        RCHK(hipMemcpyAsync(L.rb, alive, R * sizeof(int), hipMemcpyDeviceToHost, L.st));
+        RCHK(hipMemcpyAsync(L.rb + R, L.cnt + (cur ^ 1), sizeof(int), hipMemcpyDeviceToHost, L.st));
+        RCHK(hipEventRecord(L.ev_rb, L.st));
+        L.pending = true;
+        L.cur ^= 1;
+        s.world_rays += n;
+        s.trace_launches += 1;
+        s.bounces += 1;
+        progress = true;
+      }
+    }
+    // accumulate finished batches strictly in batch order, on the acc stream
+    while (acc_head < next_batch && b_done[acc_head]) {
+      Lane& L = r->lanes[b_lane[acc_head]];
+      int rg = b_reg[acc_head];
+      BatchInfo& B = batches[acc_head];
+      RCHK(hipStreamWaitEvent(ast, L.done_ev[rg], 0));
+      launch_accumulate(L.P, B, r->acc, ast);
+      if (keep) {  // region paths are [pixel][sample-in-batch]; the frame keeps [pixel][spp]
+        int np = B.n_paths / B.spp_batch, Sb = B.spp_batch;
+        RCHK(hipMemcpy2DAsync(r->raw_all + 3 * ((size_t)B.p0 * p->spp + B.s0), 3 * sizeof(float) * p->spp,
+                              L.P.raw + 3 * (size_t)B.slot0, 3 * sizeof(float) * Sb, 3 * sizeof(float) * Sb, np,
+                              hipMemcpyDeviceToDevice, ast));
+        RCHK(hipMemcpy2DAsync(r->rays_all + ((size_t)B.p0 * p->spp + B.s0), p->spp, L.P.rays + B.slot0, Sb, Sb, np,
+                              hipMemcpyDeviceToDevice, ast));
+      }
+      RCHK(hipEventRecord(L.acc_ev[rg], ast));
+      L.acc_pending[rg] = true;
+      L.reg_batch[rg] = -1;
+      ++acc_head;
+      progress = true;
+    }
+    if (!progress) std::this_thread::yield();
+  }
+  launch_finish(r->acc, d_mean, npix, p->spp, ast);
+  RCHK(hipEventRecord(r->ev_end, ast));
+  RCHK(hipStreamSynchronize(ast));
+  RCHK(hipGetLastError());
+  float total = 0;
+  RCHK(hipEventElapsedTime(&total, r->ev_beg, r->ev_end));
+  s.total_ms = total;
+  for (int l = 0; l < lanes; ++l) {
+    s.trace_ms += r->lanes[l].trace_ms;
+    s.shade_ms += r->lanes[l].shade_ms;
+  }
+  if (stats) *stats = s;
+  return 0;
+}
+
+}  // namespace srr
+
+srr_renderer::~srr_renderer() {
+  (void)hipSetDevice(device);
+  (void)hipDeviceSynchronize();
+  for (void* p : scene_bufs) (void)hipFree(p);
+  for (auto& L : lanes) {
+    srr::free_lane_paths(L);
+    (void)hipFree(L.cnt);
+    if (L.rb) (void)hipHostFree(L.rb);
+    for (hipEvent_t e : {L.ev_t0, L.ev_t1, L.ev_s1, L.ev_rb})
+      if (e) (void)hipEventDestroy(e);
+    for (int k = 0; k < srr::kRegionsPerLane; ++k) {
+      if (L.done_ev[k]) (void)hipEventDestroy(L.done_ev[k]);
+      if (L.acc_ev[k]) (void)hipEventDestroy(L.acc_ev[k]);
+    }
+    if (L.st) (void)hipStreamDestroy(L.st);
+  }
+  (void)hipFree(acc);
+  (void)hipFree(pixels);
+  (void)hipFree(sobol);
+  (void)hipFree(raw_all);
+  (void)hipFree(rays_all);
+  if (ev_beg) (void)hipEventDestroy(ev_beg);
+  if (ev_end) (void)hipEventDestroy(ev_end);
+  if (acc_st) (void)hipStreamDestroy(acc_st);
+}

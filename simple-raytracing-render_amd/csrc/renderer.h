@@ -1,0 +1,76 @@
+// The device-resident renderer behind srr_renderer_* (include/srr_capi.h):
+// uploaded scene tables plus the wavefront path pools.
+//
+// Work is organised in LANES: each lane owns a HIP stream and a pool of path
+// slots split into regions; a region holds one batch (a pixel chunk x sample
+// chunk).  A lane runs trace -> shade (material-sorted) bounces over all its live
+// paths, refilling freed regions with new batches, so a batch's tail of long
+// paths overlaps the next batches' first bounces; several lanes run
+// concurrently so one lane's straggler waves overlap other lanes' kernels.
+// Finished batches are accumulated on a separate stream strictly in batch order
+// (per-pixel sums stay in sample order, hence bitwise reproducible).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/srr_capi.h"
+#include "kernels.h"
+#include "scene.h"
+
+namespace srr {
+
+constexpr int kRegionsPerLane = 3;  // <= kernels.hip kMaxRegions
+constexpr int kMaxLanes = 4;
+
+struct Lane {
+  hipStream_t st = nullptr;
+  hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr, ev_s1 = nullptr, ev_rb = nullptr;
+  hipEvent_t done_ev[kRegionsPerLane] = {};  // batch in region finished (lane stream)
+  hipEvent_t acc_ev[kRegionsPerLane] = {};   // batch in region accumulated (acc stream)
+  bool acc_pending[kRegionsPerLane] = {};    // region reuse must wait for acc_ev
+  PathState P{};
+  int32_t* act[2] = {nullptr, nullptr};
+  int32_t* lists = nullptr;  // 4 material-family lists
+  int32_t* cnt = nullptr;    // [0..1] active counts, [2..2+R) region survivors, [2+R..6+R) families
+  int32_t* rb = nullptr;     // pinned host mirror of region survivors + next count
+  size_t cap = 0;
+  int cap_depth = 0;
+  bool has_raw = false;
+  std::vector<void*> bufs;
+  // per-frame state
+  int n = 0, cur = 0;
+  bool pending = false;
+  int reg_batch[kRegionsPerLane];
+  double trace_ms = 0, shade_ms = 0;
+};
+
+}  // namespace srr
+
+struct srr_renderer {
+  int device = 0;
+  srr::SceneView view{};
+  std::vector<void*> scene_bufs;
+  int n_lanes = 2;
+  srr::Lane lanes[srr::kMaxLanes];
+  hipStream_t acc_st = nullptr;
+  hipEvent_t ev_beg = nullptr, ev_end = nullptr;
+  // frame buffers
+  float* acc = nullptr;
+  int32_t* pixels = nullptr;
+  size_t pix_cap = 0;
+  double* sobol = nullptr;
+  int sobol_n = 0;
+  float* raw_all = nullptr;
+  uint8_t* rays_all = nullptr;
+  size_t keep_cap = 0;
+  int64_t kept_paths = 0;
+  ~srr_renderer();
+};
+
+namespace srr {
+int renderer_create(const Scene& s, int device, srr_renderer** out, std::string& err);
+int render_device(srr_renderer* r, const srr_params* p, const int32_t* pix, int64_t npix, float* d_mean,
+                  srr_stats* stats, std::string& err);
+}  // namespace srr

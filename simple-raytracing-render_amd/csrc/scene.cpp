@@ -611,14 +611,26 @@ struct Flattener {
     m.tri_off = (int)(F.tri_shade.size());
     m.n_nodes = (int)B.nodes.size();
     m.n_tris = (int)B.leaves.size();
-    for (const HBvh::Node& n : B.nodes) {
-      auto enc = [&](int c) -> int32_t { return c >= 0 ? c + m.node_off : ~(~c + m.tri_off); };
-      int32_t L = enc(n.left), R = enc(n.right);
-      float lf, rf;
-      std::memcpy(&lf, &L, 4);
-      std::memcpy(&rf, &R, 4);
-      F.node_lo.insert(F.node_lo.end(), {n.box.mn[0], n.box.mn[1], n.box.mn[2], lf});
-      F.node_hi.insert(F.node_hi.end(), {n.box.mx[0], n.box.mx[1], n.box.mx[2], rf});
+    // Threaded (stackless) layout: HBvh nodes are already in preorder with the
+    // left child at i + 1; skip[i] = i + size(subtree i) is where a traversal
+    // goes when it is done with, or prunes, node i.  Leaves record their 1-2
+    // triangles (consecutive in DFS leaf order) as (first << 1) | (count - 1).
+    std::vector<int> size(B.nodes.size(), 1);
+    for (int i = (int)B.nodes.size() - 1; i >= 0; --i)
+      if (B.nodes[i].left >= 0) size[i] = 1 + size[B.nodes[i].left] + size[B.nodes[i].right];
+    for (size_t i = 0; i < B.nodes.size(); ++i) {
+      const HBvh::Node& n = B.nodes[i];
+      int32_t skip = m.node_off + (int32_t)i + size[i];
+      int32_t leaf = -1;
+      if (n.left < 0) {
+        int first = ~n.left, last = ~n.right;
+        leaf = ((first + m.tri_off) << 1) | (last != first ? 1 : 0);
+      }
+      float sf, lf;
+      std::memcpy(&sf, &skip, 4);
+      std::memcpy(&lf, &leaf, 4);
+      F.node_lo.insert(F.node_lo.end(), {n.box.mn[0], n.box.mn[1], n.box.mn[2], sf});
+      F.node_hi.insert(F.node_hi.end(), {n.box.mx[0], n.box.mx[1], n.box.mx[2], lf});
     }
     for (int l : B.leaves) {
       const HTri& t = S.tris[S.obj[l].tri];

@@ -1,0 +1,51 @@
+"""Per-world-ray traversal counts of the REFERENCE algorithm (N_node box tests,
+N_tri triangle tests, N_prim analytic primitive tests; light-pdf probes
+excluded) and the algorithmic bytes per sample they imply:
+
+    B_cfg = 64 + 32*N_node + 36*N_tri + 32*N_prim
+
+Counted by the CPU restatement (oracle/restate.cpp), which test_oracle_pins.py
+pins bit-exact to the reference.  Writes tests/golden/traversal_counts.json.
+
+    python tests/golden/make_counts.py
+"""
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "simple-raytracing-render_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import oracle_bind as ob  # noqa: E402
+from srr import scenes  # noqa: E402
+
+CONFIGS = {
+    "C1": (scenes.s1_cornell, 96, 96, 16),
+    "C2": (scenes.s2_cornell_teapot, 96, 96, 16),
+    "C3": (scenes.s3_cornell_teapot_microfacet, 96, 96, 16),
+    "C3_metal": (lambda: scenes.s3_cornell_teapot_microfacet("metal"), 96, 96, 16),
+    "C4": (scenes.s4_soldier_standin, 192, 108, 8),
+    "C5": (scenes.s5_soldier_fog, 192, 108, 8),
+}
+
+
+def main():
+    out = {}
+    for name, (fac, nx, ny, spp) in CONFIGS.items():
+        sc, _ = fac()
+        r = ob.render(sc.text(), nx, ny, spp, 50, threads=os.cpu_count() or 4, want_paths=False)
+        w, node, tri, prim = (int(x) for x in r["stats"])
+        paths = nx * ny * spp
+        n_node, n_tri, n_prim = node / w, tri / w, prim / w
+        out[name] = dict(sample=f"{nx}x{ny}x{spp}", paths=paths, world_rays=w, rays_per_path=w / paths,
+                         N_node=n_node, N_tri=n_tri, N_prim=n_prim,
+                         B_cfg=64 + 32 * n_node + 36 * n_tri + 32 * n_prim)
+        print(name, out[name])
+    with open(os.path.join(HERE, "traversal_counts.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()
