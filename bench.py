@@ -5,10 +5,12 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \\
         --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
 
-One step = one whole frame: every rank renders its round-robin share of 32x32
-tiles through the C-ABI (srr_render_device, inputs resident in
-HBM), then the per-pixel means are gathered to rank 0 over RCCL (one
-all_gather at frame end) and assembled.  A "sample" is one world ray segment
+One step = one whole frame through the C-ABI (srr_render_device, inputs
+resident in HBM) on every rank, then the frame-end exchange over RCCL
+(srr/dist.py).  Default plan "samples" (weak scaling): each GPU
+renders the BASELINE config's 512x512x1024 paths as its sample range of one
+N*1024-spp frame; one reduce of per-pixel sums to rank 0.  Plan "tiles"
+(strong scaling): 32x32 tiles round-robin, one all_gather.  A "sample" is one world ray segment
 (one reference world->hit call).  Rank 0 prints one JSON line.
 """
 from __future__ import annotations
@@ -36,8 +38,11 @@ def parse():
     ap.add_argument("--ny", type=int, default=0)
     ap.add_argument("--spp", type=int, default=0)
     ap.add_argument("--batch-paths", type=int, default=0)
+    ap.add_argument("--plan", default="samples", choices=["samples", "tiles"],
+                    help="multi-GPU split: samples = weak scaling (each GPU renders spp samples of every "
+                         "pixel, one reduce), tiles = strong scaling (32x32 tiles round-robin, one all_gather)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
     return ap.parse_args()
 
 
@@ -53,11 +58,12 @@ def cpu_baseline(text, nx, ny, spp, budget_s):
     threads = min(16, os.cpu_count() or 1)
     rng = np.random.default_rng(1)
     # calibrate on a small sample, then size the timed sample to ~budget_s
-    cal = np.sort(rng.choice(nx * ny, size=256, replace=False)).astype(np.int32)
+    n_cal = min(nx * ny, 4096)
+    cal = np.sort(rng.choice(nx * ny, size=n_cal, replace=False)).astype(np.int32)
     t0 = time.perf_counter()
     r = ob.render(text, nx, ny, spp, 50, pixels=cal, threads=threads, want_paths=False)
     dt = max(time.perf_counter() - t0, 1e-3)
-    n = int(min(nx * ny, max(256, 256 * budget_s / dt)))
+    n = int(min(nx * ny, max(n_cal, n_cal * budget_s / dt)))
     pix = np.sort(rng.choice(nx * ny, size=n, replace=False)).astype(np.int32)
     t0 = time.perf_counter()
     r = ob.render(text, nx, ny, spp, 50, pixels=pix, threads=threads, want_paths=False)
@@ -74,6 +80,7 @@ def main():
     import torch.distributed as dist
 
     from srr import capi, scenes
+    from srr import dist as dist_frame
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -90,29 +97,13 @@ def main():
     nx, ny, spp = a.nx or cfg["nx"], a.ny or cfg["ny"], a.spp or cfg["spp"]
     text = sc.text()
     rend = capi.Renderer(text, device=local)
-    params = capi.make_params(nx, ny, spp, cfg["max_depth"], shard=(rank, world), tile=32,
-                              batch_paths=a.batch_paths)
-    my_pix = torch.from_numpy(capi.shard_pixels(params)).to(dev)
-    n_my = my_pix.numel()
-    counts = [0] * world
-    for k in range(world):
-        counts[k] = capi.shard_pixels(capi.make_params(nx, ny, spp, shard=(k, world), tile=32)).size
-    n_max = max(counts)
-    mean = torch.zeros((n_max, 3), dtype=torch.float32, device=dev)
-    gathered = [torch.zeros_like(mean) for _ in range(world)]
-    all_pix = [torch.from_numpy(capi.shard_pixels(capi.make_params(nx, ny, spp, shard=(k, world), tile=32))).to(dev)
-               for k in range(world)]
-    image = torch.zeros((nx * ny, 3), dtype=torch.float32, device=dev)
+    sh = dist_frame.plan_shard(nx, ny, spp, cfg["max_depth"], rank, world, plan=a.plan, tile=32,
+                               batch_paths=a.batch_paths)
+    ex = dist_frame.FrameExchange(sh, dev, dist if world > 1 else None)
 
     def step():
-        st = rend.render_device(params, mean.data_ptr())
-        if world > 1:
-            dist.all_gather(gathered, mean)  # the frame-end exchange over RCCL / xGMI
-            if rank == 0:
-                for k in range(world):
-                    image[all_pix[k]] = gathered[k][:counts[k]]
-        else:
-            image[my_pix] = mean[:n_my]
+        st = rend.render_device(sh.params, ex.local.data_ptr())
+        ex.finish()  # frame-end exchange (RCCL) + assembly on rank 0
         return st
 
     def barrier():
@@ -165,14 +156,18 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": round(elapsed / a.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "weak" if a.plan == "samples" else "strong",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (scene built in code: Cornell box + tessellated Utah teapot)",
-            "config": {"workload": f"{key}: {a.scene} {nx}x{ny} {spp}spp maxDepth {cfg['max_depth']}, "
-                                   f"32x32 tiles round-robin over {world} GPU(s), RCCL all_gather at frame end",
-                       "nx": nx, "ny": ny, "spp": spp, "world_rays_per_step": int(rays_total / a.steps),
-                       "parallelism": f"tiles{world}"},
+            "config": {"workload": f"{key}: {a.scene} {nx}x{ny} {spp}spp maxDepth {cfg['max_depth']}" + (
+                                   f", 32x32 tiles round-robin over {world} GPU(s), RCCL all_gather at frame end"
+                                   if a.plan == "tiles" else
+                                   f" per GPU; {world} GPU(s) render sample ranges of one {spp * world}spp frame, "
+                                   f"RCCL reduce at frame end"),
+                       "nx": nx, "ny": ny, "spp_per_gpu" if a.plan == "samples" else "spp": spp,
+                       "frame_spp": sh.total_spp, "world_rays_per_step": int(rays_total / a.steps),
+                       "parallelism": f"{a.plan}{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                          "traffic": traffic, "kernel": "srr_trace (k_trace)", "B_cfg": round(b_cfg, 1),

@@ -103,7 +103,6 @@ int srr_bvh_node(srr_scene* s, const int* children, int n, float time0, float ti
 /* Utah teapot (teapot.h:76-166) with `divs` subdivisions: creates 2*32*divs^2
  * triangle handles, first_handle .. first_handle+count-1, returns count. */
 int srr_teapot(srr_scene* s, float scale, int divs, int mat, int* first_handle);
-/* Handles of [first, first+count) as an array for list/bvh constructors. */
 
 /* camera.h:33-48, 9-argument constructor */
 int srr_camera(srr_scene* s, const float lookfrom[3], const float lookat[3], const float vup[3], float vfov,
@@ -124,6 +123,8 @@ typedef struct srr_params {
   int batch_paths;     /* paths in flight per wavefront batch (0 = auto)       */
   uint64_t base_seed;  /* per-path seed salt; 0 = SURVEY §8(d) definition      */
   int flags;           /* SRR_FLAG_*                                           */
+  int sample_begin;    /* global index of sample 0: a sample shard renders     */
+                       /*   samples [sample_begin, sample_begin + spp)         */
 } srr_params;
 
 #define SRR_FLAG_SORT_MATERIALS 1 /* material-sorted shading (perf only)      */
@@ -150,8 +151,9 @@ int64_t srr_shard_pixels(const srr_params* p, int32_t* pixel_index);
  * in srr_shard_pixels() order.  Inputs are resident on the device; the call
  * returns after the device work finished. */
 int srr_render_device(srr_renderer* r, const srr_params* p, float* d_mean, srr_stats* stats);
-/* Host convenience: whole image (shard 0 of 1), mean (nx*ny*3, may be NULL)
- * and 8-bit tone-mapped rgb8 (nx*ny*3, Raytracing_n.cpp:850-867, may be NULL). */
+/* Host convenience (the CRender::Run of Render.h:16-51): the shard's pixels
+ * (the whole image when shard_count <= 1) as mean radiance (npix*3, may be NULL)
+ * and 8-bit tone-mapped rgb8 (npix*3, Raytracing_n.cpp:850-867, may be NULL). */
 int srr_render(srr_renderer* r, const srr_params* p, float* mean, unsigned char* rgb8, srr_stats* stats);
 /* After a render with SRR_FLAG_KEEP_PATHS: per-path raw radiance (before
  * de_nan) and world-ray counts, [n_shard_pixels][spp]. */

@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdint>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -293,6 +294,8 @@ int64_t srr_shard_pixels(const srr_params* p, int32_t* out) {
 int srr_render_device(srr_renderer* r, const srr_params* p, float* d_mean, srr_stats* stats) {
   if (!r || !p || !d_mean) return fail(SRR_EINVAL, "null argument");
   if (p->spp < 1 || p->max_depth < 0 || p->max_depth > 64) return fail(SRR_EINVAL, "spp >= 1, 0 <= max_depth <= 64");
+  if (p->sample_begin < 0 || p->sample_begin > INT32_MAX - p->spp)
+    return fail(SRR_EINVAL, "sample_begin must be >= 0 and sample_begin + spp must fit in int32");
   int64_t npix = srr_shard_pixels(p, nullptr);
   if (npix < 0) return (int)npix;
   std::vector<int32_t> pix(npix);

@@ -56,10 +56,11 @@ struct BatchInfo {
   int act0;               // ... at this offset
   int slot0;              // first path-state slot of the batch's region
   const int32_t* pixels;  // shard pixel list (PPM-order indices)
-  const double* sobol;    // [spp][2]
+  const double* sobol;    // [spp][2], already offset to global sample s_base
   int p0;                 // first shard pixel of the batch
   int n_paths;            // pixels_in_batch * spp_batch
-  int s0, spp_batch;      // sample range [s0, s0 + spp_batch)
+  int s0, spp_batch;      // sample range [s0, s0 + spp_batch) of this render
+  int s_base;             // global index of this render's sample 0 (sample sharding)
   int nx, ny;
   uint64_t base_seed;
 };

@@ -867,7 +867,7 @@ __global__ void __launch_bounds__(256) k_raygen(SceneView S, PathState P, BatchI
   int j = B.ny - 1 - pix / B.nx;  // Raytracing_n.cpp:827-828 (SURVEY Q12 fix)
   // per-path seeding
   uint64_t h = 0xcbf29ce484222325ULL ^ B.base_seed;
-  uint32_t w[3] = {(uint32_t)i, (uint32_t)j, (uint32_t)s};
+  uint32_t w[3] = {(uint32_t)i, (uint32_t)j, (uint32_t)(B.s_base + s)};
   for (int k = 0; k < 3; ++k)
     for (int b = 0; b < 4; ++b) {
       h ^= (w[k] >> (8 * b)) & 0xffu;

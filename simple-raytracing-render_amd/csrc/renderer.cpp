@@ -165,13 +165,17 @@ int render_device(srr_renderer* r, const srr_params* p, const int32_t* pix, int6
     r->pix_cap = npix;
   }
   RCHK(hipMemcpy(r->pixels, pix, npix * sizeof(int32_t), hipMemcpyHostToDevice));
-  if (p->spp > r->sobol_n) {
+  // Sobol points of the global sample range [sample_begin, sample_begin + spp):
+  // the set is a prefix-stable sequence, so a sample shard reads its own slice.
+  const int n_sobol = p->sample_begin + p->spp;
+  if (n_sobol > r->sobol_n) {
     (void)hipFree(r->sobol);
-    RCHK(hipMalloc((void**)&r->sobol, 2 * (size_t)p->spp * sizeof(double)));
-    r->sobol_n = p->spp;
+    r->sobol = nullptr;
+    RCHK(hipMalloc((void**)&r->sobol, 2 * (size_t)n_sobol * sizeof(double)));
+    r->sobol_n = n_sobol;
   }
-  std::vector<double> sp(2 * (size_t)p->spp);
-  sobol2((unsigned)p->spp, sp.data());
+  std::vector<double> sp(2 * (size_t)n_sobol);
+  sobol2((unsigned)n_sobol, sp.data());
   RCHK(hipMemcpy(r->sobol, sp.data(), sp.size() * sizeof(double), hipMemcpyHostToDevice));
   if (keep) {
     size_t need = (size_t)npix * p->spp;
@@ -196,7 +200,8 @@ int render_device(srr_renderer* r, const srr_params* p, const int32_t* pix, int6
     for (int s0 = 0; s0 < p->spp; s0 += S) {
       BatchInfo B{};
       B.pixels = r->pixels;
-      B.sobol = r->sobol;
+      B.sobol = r->sobol + 2 * (size_t)p->sample_begin;
+      B.s_base = p->sample_begin;
       B.p0 = (int)p0;
       B.spp_batch = std::min(S, p->spp - s0);
       B.n_paths = np * B.spp_batch;

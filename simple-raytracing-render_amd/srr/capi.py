@@ -24,7 +24,8 @@ class SrrError(RuntimeError):
 class Params(ctypes.Structure):
     _fields_ = [("nx", ctypes.c_int), ("ny", ctypes.c_int), ("spp", ctypes.c_int), ("max_depth", ctypes.c_int),
                 ("tile", ctypes.c_int), ("shard_index", ctypes.c_int), ("shard_count", ctypes.c_int),
-                ("batch_paths", ctypes.c_int), ("base_seed", ctypes.c_uint64), ("flags", ctypes.c_int)]
+                ("batch_paths", ctypes.c_int), ("base_seed", ctypes.c_uint64), ("flags", ctypes.c_int),
+                ("sample_begin", ctypes.c_int)]
 
 
 class Stats(ctypes.Structure):
@@ -71,8 +72,9 @@ def _ptr(a):
     return None if a is None else a.ctypes.data
 
 
-def make_params(nx, ny, spp, max_depth=50, shard=(0, 1), tile=32, batch_paths=0, base_seed=0, flags=0):
-    return Params(nx, ny, spp, max_depth, tile, shard[0], shard[1], batch_paths, base_seed, flags)
+def make_params(nx, ny, spp, max_depth=50, shard=(0, 1), tile=32, batch_paths=0, base_seed=0, flags=0,
+                sample_begin=0):
+    return Params(nx, ny, spp, max_depth, tile, shard[0], shard[1], batch_paths, base_seed, flags, sample_begin)
 
 
 def shard_pixels(p: Params) -> np.ndarray:

@@ -1,0 +1,106 @@
+"""Multi-GPU frame rendering: one process per GPU, torch.distributed over RCCL
+(gloo on CPU for tests).  SURVEY.md §8(e).
+
+Every (pixel, sample) path is independent and the scene is read-only, so a
+frame shards with no exchange until the end.  Two plans:
+
+* ``tiles``   (strong scaling, a fixed frame): rank k renders the 32x32 tiles
+  t with t % world == k, all samples.  Frame end: one all_gather of the packed
+  per-pixel means; rank 0 scatters them into the image.  Bitwise equal to the
+  one-GPU image (each pixel's samples are summed on one GPU in sample order).
+* ``samples`` (weak scaling, fixed work per GPU): rank k renders every pixel
+  with samples [k*spp, (k+1)*spp) of one frame of world*spp samples per pixel
+  (the per-path seeds and Sobol points are the global sample index's, so
+  rank 0's slice is exactly the one-GPU spp frame).  Frame end: one reduce of
+  the per-pixel sample sums to rank 0.  Equal to the one-GPU world*spp frame up
+  to float summation order (partial sums per rank).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import capi
+
+PLANS = ("tiles", "samples")
+
+
+@dataclass
+class Shard:
+    rank: int
+    world: int
+    plan: str
+    params: capi.Params          # what this rank renders
+    pixels: np.ndarray           # PPM-order pixel indices this rank outputs (ascending)
+    counts: list                 # pixels per rank (tiles) / frame pixels (samples)
+    total_spp: int               # samples per pixel of the assembled frame
+
+
+def plan_shard(nx, ny, spp, max_depth, rank, world, plan="tiles", tile=32, batch_paths=0, flags=0) -> Shard:
+    """Split one frame over `world` ranks.  `spp` is the frame's samples per
+    pixel for ``tiles`` and the per-rank samples per pixel for ``samples``."""
+    if plan not in PLANS:
+        raise ValueError(f"plan must be one of {PLANS}")
+    if not 0 <= rank < world:
+        raise ValueError("rank out of range")
+    if plan == "tiles":
+        p = capi.make_params(nx, ny, spp, max_depth, shard=(rank, world), tile=tile, batch_paths=batch_paths,
+                             flags=flags)
+        counts = [capi.shard_pixels(capi.make_params(nx, ny, spp, shard=(k, world), tile=tile)).size
+                  for k in range(world)]
+        return Shard(rank, world, plan, p, capi.shard_pixels(p), counts, spp)
+    p = capi.make_params(nx, ny, spp, max_depth, shard=(0, 1), tile=tile, batch_paths=batch_paths, flags=flags,
+                         sample_begin=rank * spp)
+    return Shard(rank, world, plan, p, np.arange(nx * ny, dtype=np.int32), [nx * ny] * world, spp * world)
+
+
+def shard_pixels_of(sh: Shard, k: int) -> np.ndarray:
+    """Pixel list of rank k under the same plan (rank 0 scatters with these)."""
+    if sh.plan == "samples":
+        return sh.pixels
+    p = capi.make_params(sh.params.nx, sh.params.ny, sh.params.spp, shard=(k, sh.world), tile=sh.params.tile)
+    return capi.shard_pixels(p)
+
+
+class FrameExchange:
+    """Frame-end exchange for one plan, with buffers allocated once.
+
+    `local` is this rank's [n_max, 3] float32 tensor of per-pixel means (rows
+    beyond its pixel count are ignored).  `finish()` returns the assembled
+    [nx*ny, 3] frame of means on rank 0 (None elsewhere)."""
+
+    def __init__(self, sh: Shard, device, dist=None):
+        import torch
+        self.sh, self.dist, self.torch = sh, dist, torch
+        nx, ny = sh.params.nx, sh.params.ny
+        self.n_max = max(sh.counts)
+        self.local = torch.zeros((self.n_max, 3), dtype=torch.float32, device=device)
+        self.image = torch.zeros((nx * ny, 3), dtype=torch.float32, device=device)
+        if sh.plan == "tiles":
+            self.gathered = [torch.zeros_like(self.local) for _ in range(sh.world)]
+            self.idx = [torch.from_numpy(shard_pixels_of(sh, k).astype(np.int64)).to(device)
+                        for k in range(sh.world)]
+
+    def finish(self):
+        sh, torch = self.sh, self.torch
+        if sh.world == 1:
+            if sh.plan == "tiles":
+                self.image[self.idx[0]] = self.local[:sh.counts[0]]
+            else:
+                self.image.copy_(self.local)
+            return self.image
+        if sh.plan == "tiles":
+            self.dist.all_gather(self.gathered, self.local)  # one exchange over RCCL / xGMI
+            if sh.rank != 0:
+                return None
+            for k in range(sh.world):
+                self.image[self.idx[k]] = self.gathered[k][:sh.counts[k]]
+            return self.image
+        # samples: per-pixel sums of this rank's samples, reduced to rank 0
+        self.local.mul_(float(sh.params.spp))
+        self.dist.reduce(self.local, dst=0)
+        if sh.rank != 0:
+            return None
+        torch.div(self.local, float(sh.total_spp), out=self.image)
+        return self.image

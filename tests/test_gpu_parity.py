@@ -57,6 +57,19 @@ def test_shards_assemble_to_the_same_image():
     np.testing.assert_array_equal(asm.view(np.uint32), full.view(np.uint32))
 
 
+def test_sample_shards_are_slices_of_the_full_render():
+    """Sample sharding (srr/dist.py plan "samples"): a render of samples
+    [b, b + n) is bitwise the same paths as that slice of the full render."""
+    sc, _ = scenes.s2_cornell_teapot()
+    r = capi.Renderer(sc.text())
+    nx, ny, spp = 32, 24, 6
+    full = r.render(nx, ny, spp, 50, keep_paths=True)
+    for b, n in ((0, 2), (2, 3), (5, 1)):
+        part = r.render(nx, ny, n, 50, keep_paths=True, sample_begin=b)
+        np.testing.assert_array_equal(part["paths"].view(np.uint32), full["paths"][:, b:b + n].view(np.uint32))
+        np.testing.assert_array_equal(part["rays"], full["rays"][:, b:b + n])
+
+
 def test_batch_size_does_not_change_the_image():
     sc, _ = scenes.s3_cornell_teapot_microfacet()
     r = capi.Renderer(sc.text())

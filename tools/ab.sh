@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B bench variants on one box: tools_ab.sh TAG "ENV1" "ENV2" ...
+# A/B bench variants on one box: tools/ab.sh TAG "ENV1" "ENV2" ...
 TAG=$1; shift
 timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/$TAG.tests.log 2>&1
 echo "tests rc=$?"; tail -1 gpurun_out/$TAG.tests.log

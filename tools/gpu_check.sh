@@ -1,5 +1,5 @@
 #!/bin/bash
-# usage: tools_gpu_check.sh TAG  -- GPU tests, bench, kernel-trace profile (run via gpurun)
+# usage: tools/gpu_check.sh TAG  -- GPU tests, bench, kernel-trace profile (run via gpurun)
 TAG=${1:-run}
 R=$PWD
 timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/$TAG.tests.log 2>&1
