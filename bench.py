@@ -42,6 +42,7 @@ def parse():
                     help="multi-GPU split: samples = weak scaling (each GPU renders spp samples of every "
                          "pixel, one reduce), tiles = strong scaling (32x32 tiles round-robin, one all_gather)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--count-visits", action="store_true", help="diagnostic: count mesh box/triangle tests (slower)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     return ap.parse_args()
 
@@ -98,7 +99,7 @@ def main():
     text = sc.text()
     rend = capi.Renderer(text, device=local)
     sh = dist_frame.plan_shard(nx, ny, spp, cfg["max_depth"], rank, world, plan=a.plan, tile=32,
-                               batch_paths=a.batch_paths)
+                               batch_paths=a.batch_paths, flags=capi.FLAG_COUNT_VISITS if a.count_visits else 0)
     ex = dist_frame.FrameExchange(sh, dev, dist if world > 1 else None)
 
     def step():
@@ -118,8 +119,10 @@ def main():
     rays = 0
     trace_ms = 0.0
     launches = 0
+    visits = [0, 0, 0]
     for _ in range(a.steps):
         st = step()
+        visits = [visits[0] + st["box_tests"], visits[1] + st["tri_tests"], visits[2] + st["stack_overflows"]]
         rays += st["world_rays"]
         trace_ms += st["trace_ms"]
         launches += st["trace_launches"]
@@ -173,6 +176,9 @@ def main():
                          "traffic": traffic, "kernel": "srr_trace (k_trace)", "B_cfg": round(b_cfg, 1),
                          "trace_ms_per_launch": round(trace_ms / max(launches, 1), 4)},
         }
+        if a.count_visits:
+            out["visits"] = {"box_tests_per_ray": visits[0] / max(rays, 1), "tri_tests_per_ray": visits[1] / max(rays, 1),
+                             "stack_overflows": visits[2], "note": "counting run: timing not representative"}
         if world == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(text, nx, ny, spp, a.cpu_seconds)
         print(json.dumps(out), flush=True)

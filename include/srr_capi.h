@@ -129,6 +129,7 @@ typedef struct srr_params {
 
 #define SRR_FLAG_SORT_MATERIALS 1 /* material-sorted shading (perf only)      */
 #define SRR_FLAG_KEEP_PATHS 2     /* keep per-path radiance for parity tests   */
+#define SRR_FLAG_COUNT_VISITS 4   /* count mesh box / triangle tests (slower)    */
 
 typedef struct srr_stats {
   int64_t world_rays;   /* world->hit calls (the metric's samples)             */
@@ -138,6 +139,10 @@ typedef struct srr_stats {
   double shade_ms;
   double total_ms;      /* render wall time on the device stream               */
   int64_t bounces;      /* bounce iterations launched                          */
+  int64_t box_tests;    /* SRR_FLAG_COUNT_VISITS: mesh BVH boxes tested        */
+  int64_t tri_tests;    /*   triangle tests (a 1-triangle leaf counts 2, as    */
+                        /*   the reference tests it twice, bvh.h:104-105)      */
+  int64_t stack_overflows; /* rays re-walked on the stackless BVH2             */
 } srr_stats;
 
 /* Flatten the scene and upload it to HIP device `device`. */

@@ -6,12 +6,19 @@
 //                                           inlined in order, instance wrappers
 //                                           distributed onto each child as a
 //                                           transform chain (xforms[])
-//   mesh BVH       float4 node_lo/hi[N]     reference-topology BVH2 (bvh.h:96-119) in
-//                                           preorder, threaded for stackless traversal:
+//   mesh BVH       float4 nodes[2N]         reference-topology BVH2 (bvh.h:96-119) in
+//                                           preorder, threaded for stackless traversal,
+//                                           one 32-B record per node (half a cache line):
 //                                           lo = (min.xyz, skip), hi = (max.xyz, leaf)
 //                                           skip = next node once this subtree is done;
 //                                           leaf = (first_tri << 1) | (count - 1), or -1
-//   triangles      float4 tri_pos[3*T]      p0, p1, p2 in BVH leaf (DFS) order
+//   mesh BVH4      float4 node4[8*N4]       the same BVH collapsed to 4-wide nodes: each
+//                                           node holds up to 4 reference nodes' boxes
+//                                           (SoA: lo.x[4], lo.y[4], lo.z[4], hi.x[4],
+//                                           hi.y[4], hi.z[4]) and child refs (int4):
+//                                           >= 0 node4 index, < 0 ~leaf code, INT32_MIN
+//                                           empty slot; 128 B
+//   triangles      float4 tri_pos[4*T]      p0, p1, p2, pad (one 64-B line) in BVH leaf (DFS) order
 //                  TriShade tri_shade[T]    n0..n2, uv0..uv2, material
 //   materials/textures/images/lights/camera   small tables
 //
@@ -65,6 +72,8 @@ struct DMesh {
   int32_t node_off;  // into node arrays (root = node_off)
   int32_t tri_off;   // into tri arrays
   int32_t n_nodes, n_tris;
+  int32_t node4_off; // root of the 4-wide view in node4[]
+  int32_t n_node4;
 };
 
 struct DMedium {  // constant_medium.h:4-50

@@ -51,6 +51,29 @@ SRR_D T cload(const T* p, int i) {
   return v;
 }
 
+// Path-state streams are loaded and stored nontemporal so the scene (BVH nodes,
+// triangles: ~1 MB) keeps its place in each XCD's L2.
+template <class T>
+SRR_D T ntl(const T* p) { return __builtin_nontemporal_load(p); }
+template <class T>
+struct NtId {
+  typedef T type;
+};
+template <class T>
+SRR_D void nts(T* p, typename NtId<T>::type v) { __builtin_nontemporal_store(v, p); }
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+SRR_D float4 ntl(const float4* p) {
+  f32x4 v = __builtin_nontemporal_load((const f32x4*)p);
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
+SRR_D void nts(float4* p, float4 x) { __builtin_nontemporal_store(f32x4{x.x, x.y, x.z, x.w}, (f32x4*)p); }
+SRR_D int4 ntl(const int4* p) {
+  i32x4 v = __builtin_nontemporal_load((const i32x4*)p);
+  return make_int4(v[0], v[1], v[2], v[3]);
+}
+SRR_D void nts(int4* p, int4 x) { __builtin_nontemporal_store(i32x4{x.x, x.y, x.z, x.w}, (i32x4*)p); }
+
 // vec3.h: float x3 value type; every operator is the reference's per-component op
 struct V3 {
   float x, y, z;

@@ -18,9 +18,9 @@ struct SceneView {  // device pointers into the flattened tables (device_scene.h
   const DRect* rects;
   const DStandaloneTri* stris;
   const DMesh* meshes;
-  const float4* node_lo;
-  const float4* node_hi;
-  const float4* tri_pos;
+  const float4* nodes;  // 2 float4 per BVH2 node: lo (min.xyz, skip), hi (max.xyz, leaf)
+  const float4* node4;  // 8 float4 per 4-wide node (device_scene.h)
+  const float4* tri_pos;  // 4 float4 per triangle: p0, p1, p2, pad
   const TriShade* tri_shade;
   const DMedium* media;
   const DMat* mats;
@@ -31,6 +31,12 @@ struct SceneView {  // device pointers into the flattened tables (device_scene.h
   const DLight* lights;
   int n_lights;
   const DCamera* cam;
+  // the world traversal's tables packed in one blob (16-B aligned pieces) that
+  // the trace kernel copies to LDS when it is small: byte offsets of objs,
+  // xforms, spheres, rects, stris, meshes, media
+  const uint4* world_blob;
+  int world_words;  // 16-B words
+  int world_off[7];
 };
 
 // Struct-of-arrays state of the paths of one batch (capacity N).
@@ -41,9 +47,9 @@ struct PathState {
   uint64_t* pcg;    // PCG32 state (pdf.h:20), per path
   int32_t* depth;   // the reference's *depth
   uint64_t* spec;   // bit k: bounce k was specular
-  float4* hit_p;    // p.xyz, u
-  float4* hit_n;    // normal.xyz, v
-  int32_t* hit_mat; // material row, -1 null material, -2 miss
+  int4* hit_w;      // closest hit: object (-1 miss), primitive, t (float bits), material (-1 null)
+  float4* hit_p;    // its record (k_record): p.xyz, u
+  float4* hit_n;    //   normal.xyz, v
   float4* rec_a;    // [path][max_depth]: attenuation*scattering_pdf (or attenuation), pdf
   float* sample;    // [path][3] de_nan'd radiance
   float* raw;       // [path][3] radiance before de_nan (optional)
@@ -65,9 +71,11 @@ struct BatchInfo {
   uint64_t base_seed;
 };
 
+void dump_trace_timing();
 void launch_raygen(const SceneView& S, const PathState& P, const BatchInfo& B, hipStream_t st);
 void launch_trace(const SceneView& S, const PathState& P, const int* active, const int* count, int max_n,
-                  int* lists, int list_cap, int* fam_count, int max_depth, uint32_t* ctr, hipStream_t st);
+                  int* lists, int list_cap, int* fam_count, int* fetch, int max_depth, unsigned long long* ctr,
+                  hipStream_t st);
 void launch_shade(const SceneView& S, const PathState& P, const int* lists, int list_cap, const int* fam_count,
                   int* next, int* next_count, int* region_alive, int region_size, int max_n, int max_depth,
                   hipStream_t st);

@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdlib>
+#include <cstring>
 
 #include "device_scene.h"
 #include "devmath.h"
@@ -89,6 +90,9 @@ SRR_D bool tri_hit(V3 p0, V3 p1, V3 p2, bool front, V3 o, V3 dir, float& t, floa
   return true;
 }
 
+// Triangles are padded to 64 B (kTriStride float4) so a test touches one cache line.
+constexpr int kTriStride = 4;
+
 // aabb.h:33-49 with the per-axis reciprocal hoisted (same value each test).
 // Branchless: the reference returns false at the first axis with tmax <= tmin;
 // tmin only grows and tmax only shrinks over the axes (NaN slabs leave both
@@ -113,6 +117,16 @@ struct MeshHit {
   int tri;
 };
 
+// bvh.h:83-86 reduces the two subtrees' hits with `left.t < right.t ? left :
+// right`.  Over leaves in DFS order that is a left fold in which a later
+// triangle replaces the current one unless current.t < later.t: the smallest t
+// with ties to the later triangle, and -- for a NaN ray, whose every triangle
+// test yields t = NaN -- the last triangle.  `wins` applies that fold for a
+// candidate met in any order (ti is the DFS position).
+SRR_D bool wins(float t, int ti, float best_t, int best_i) {
+  return ti > best_i ? !(best_t < t) : (t < best_t);
+}
+
 // bvh.h:64-93 over the reference-topology BVH: a node is tested against the
 // incoming [tmin, tmax] (never shrunk: the reference tests both children with
 // the same t_max), and among the tested triangles that hit, the smallest t wins,
@@ -122,7 +136,7 @@ struct MeshHit {
 // next node (the left child); box miss or leaf done -> the skip link.
 template <bool PREFETCH>
 SRR_D bool mesh_hit(const SceneView& S, const DMesh& m, const Ray& r, float tmin, float tmax, bool is_medium,
-                    MeshHit& out, uint32_t* ctr) {
+                    MeshHit& out, unsigned long long* ctr) {
   V3 inv = v3(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
   V3 dir = r.d / length(r.d);
   int node = m.node_off;
@@ -131,7 +145,7 @@ SRR_D bool mesh_hit(const SceneView& S, const DMesh& m, const Ray& r, float tmin
   float best_t = 0;
   int best_i = -1;
   uint32_t nbox = 0, ntri = 0;
-  float4 lo = S.node_lo[node], hi = S.node_hi[node];
+  float4 lo = S.nodes[2 * (node)], hi = S.nodes[2 * (node) + 1];
   for (;;) {
     ++nbox;
     const int skip = __float_as_int(lo.w);
@@ -140,21 +154,21 @@ SRR_D bool mesh_hit(const SceneView& S, const DMesh& m, const Ray& r, float tmin
     // their latency overlaps this node's work (one-node lookahead)
     float4 lo_c, hi_c, lo_s, hi_s;
     if (PREFETCH) {
-      if (leaf < 0) { lo_c = S.node_lo[node + 1]; hi_c = S.node_hi[node + 1]; }
-      if (skip < end) { lo_s = S.node_lo[skip]; hi_s = S.node_hi[skip]; }
+      if (leaf < 0) { lo_c = S.nodes[2 * (node + 1)]; hi_c = S.nodes[2 * (node + 1) + 1]; }
+      if (skip < end) { lo_s = S.nodes[2 * (skip)]; hi_s = S.nodes[2 * (skip) + 1]; }
     }
     bool hit = slab(lo, hi, r.o, inv, tmin, tmax);
     if (hit && leaf >= 0) {
       int first = leaf >> 1, count = (leaf & 1) + 1;
       ntri += 2;  // the reference tests a one-triangle leaf twice (bvh.h:104-105)
       for (int ti = first; ti < first + count; ++ti) {
-        const float4* tp = S.tri_pos + 3 * (size_t)ti;
+        const float4* tp = S.tri_pos + kTriStride * (size_t)ti;
         float4 a = tp[0], b = tp[1], c = tp[2];
         V3 p0 = v3(a.x, a.y, a.z), p1 = v3(b.x, b.y, b.z), p2 = v3(c.x, c.y, c.z);
         float t, u, v;
         bool h = tri_hit(p0, p1, p2, true, r.o, dir, t, u, v);
         if (!h && is_medium) { ++ntri; h = tri_hit(p0, p1, p2, false, r.o, dir, t, u, v); }
-        if (h && (!found || t < best_t || (t == best_t && ti > best_i))) {
+        if (h && (!found || wins(t, ti, best_t, best_i))) {
           found = true;
           best_t = t;
           best_i = ti;
@@ -168,12 +182,182 @@ SRR_D bool mesh_hit(const SceneView& S, const DMesh& m, const Ray& r, float tmin
       lo = down ? lo_c : lo_s;
       hi = down ? hi_c : hi_s;
     } else {
-      lo = S.node_lo[next];
-      hi = S.node_hi[next];
+      lo = S.nodes[2 * (next)];
+      hi = S.nodes[2 * (next) + 1];
     }
     node = next;
   }
-  if (ctr) { atomicAdd(ctr, nbox); atomicAdd(ctr + 1, ntri); }
+  if (ctr) { atomicAdd(ctr, (unsigned long long)nbox); atomicAdd(ctr + 1, (unsigned long long)ntri); }
+  out.t = best_t;
+  out.tri = best_i;
+  return found;
+}
+
+// Traversal modes of the trace kernel (SRR_TRAVERSAL): the reference BVH2
+// threaded and stackless, or its 4-wide view (device_scene.h) near-first with an
+// LDS stack, optionally pruning subtrees by the closest hit found so far.
+enum Traversal : int { TR_BVH2 = 0, TR_BVH4 = 1, TR_BVH4_PRUNE = 2, TR_BVH4_TIMED = 3 };
+// TR | TR_WL: the world tables (objects, transforms, primitives, meshes, media)
+// were staged in LDS by the kernel, so they are read with plain (ds_read) loads
+constexpr int TR_WL = 16;
+constexpr int tr_mode(int tr) { return tr & 15; }
+template <int TR, class T>
+SRR_D T wload(const T* p, int i) {
+  if constexpr ((TR & TR_WL) != 0) return p[i];
+  else return cload(p, i);
+}
+constexpr int kTraceBlock = 256;
+constexpr int kStack = 12;
+constexpr int kWorldLdsBytes = 8192;  // world tables staged in LDS up to this size
+constexpr unsigned long long kTimingCap = 1 << 16;  // SRR_TIMING wave records  // LDS stack entries per ray; deeper -> exact BVH2 re-walk
+
+struct TraceCtx {
+  unsigned long long* ctr;  // optional counters: boxes tested, triangle tests, stack overflows
+  int* st_node;    // this thread's LDS stack (stride kTraceBlock)
+  float* st_t;     // entry distance of each stacked node
+  // SRR_TIMING diagnostics (wave-uniform): cycles inside mesh traversals, steps
+  mutable uint64_t mesh_cycles = 0;
+  mutable int mesh_steps = 0;
+};
+
+// Pruning margin: a subtree is skipped only when its box starts beyond
+// best_t * kPruneSlack along the ray.  The reference tests every leaf box the
+// ray segment [tmin, tmax] crosses and keeps the smallest triangle t (a
+// distance) with ties to the later leaf; a skipped box starts (in exact
+// arithmetic) no nearer than any triangle inside it is hit, so it could only
+// hold a hit at t > best_t unless the triangle's float t were more than 6 %
+// short of its box entry -- far beyond the few-ulp error of both computations.
+constexpr float kPruneSlack = 1.0625f;
+
+// 4-wide traversal of one mesh; same result as mesh_hit (the reference's
+// leaf set, min t, ties to the later DFS triangle).
+template <bool PRUNE, bool TIMING = false>
+SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmin, float tmax, bool is_medium,
+                     MeshHit& out, const TraceCtx& cx) {
+  const V3 inv = v3(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+  const float len = length(r.d);
+  const V3 dir = r.d / len;
+  const float to_param = kPruneSlack / len;
+  bool found = false;
+  float best_t = 0;
+  int best_i = -1;
+  float bound = tmax;
+  int node = m.node4_off;
+  int sp = 0;
+  bool overflow = false;
+  uint32_t nbox = 0, ntri = 0;
+  const uint64_t tm_enter = TIMING ? __builtin_amdgcn_s_memtime() : 0;
+  for (;;) {
+    const float4* N = S.node4 + 8 * (size_t)node;
+    const float4 LX = N[0], LY = N[1], LZ = N[2], HX = N[3], HY = N[4], HZ = N[5];
+    const int4 CH = *(const int4*)(N + 6);
+    nbox += 4;
+    float near[4];
+    bool hit[4];
+#define SRR_CHILD(c, C)                                                                  \
+  {                                                                                      \
+    float lo_ = tmin, hi_ = bound;                                                       \
+    SRR_SLAB_AX(LX.C, HX.C, r.o.x, inv.x) SRR_SLAB_AX(LY.C, HY.C, r.o.y, inv.y)          \
+    SRR_SLAB_AX(LZ.C, HZ.C, r.o.z, inv.z)                                                \
+    near[c] = lo_;                                                                       \
+    hit[c] = !(hi_ <= lo_);                                                              \
+  }
+#define SRR_SLAB_AX(L, H, O, I)                      \
+  {                                                  \
+    float t0 = (L - O) * I, t1 = (H - O) * I;        \
+    bool sw = I < 0.0f;                              \
+    float n_ = sw ? t1 : t0, f_ = sw ? t0 : t1;      \
+    lo_ = n_ > lo_ ? n_ : lo_;                       \
+    hi_ = f_ < hi_ ? f_ : hi_;                       \
+  }
+    SRR_CHILD(0, x) SRR_CHILD(1, y) SRR_CHILD(2, z) SRR_CHILD(3, w)
+#undef SRR_SLAB_AX
+#undef SRR_CHILD
+    const int ch[4] = {CH.x, CH.y, CH.z, CH.w};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      // (a NaN ray passes every slab test, as in the reference, so empty slots
+      // are told apart by their INT_MIN child, not by their inverted box)
+      if (!hit[c] || ch[c] >= 0 || ch[c] == INT32_MIN) continue;
+      const int leaf = ~ch[c];
+      const int first = leaf >> 1, count = (leaf & 1) + 1;
+      ntri += 2;
+      for (int ti = first; ti < first + count; ++ti) {
+        const float4* tp = S.tri_pos + kTriStride * (size_t)ti;
+        float4 a = tp[0], b = tp[1], cc = tp[2];
+        V3 p0 = v3(a.x, a.y, a.z), p1 = v3(b.x, b.y, b.z), p2 = v3(cc.x, cc.y, cc.z);
+        float t, u, v;
+        bool h = tri_hit(p0, p1, p2, true, r.o, dir, t, u, v);
+        if (!h && is_medium) h = tri_hit(p0, p1, p2, false, r.o, dir, t, u, v);
+        if (h && (!found || wins(t, ti, best_t, best_i))) {
+          found = true;
+          best_t = t;
+          best_i = ti;
+        }
+      }
+      // shrink only with ordered compares: a NaN bound (the reference passes
+      // every box then) or a NaN best keeps the bound as it is
+      if (PRUNE && found && best_t * to_param < bound) bound = best_t * to_param;
+    }
+    // inner children that (still) overlap [tmin, bound], nearest first
+    float kt[4];
+    int kn[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      bool take = hit[c] && ch[c] >= 0 && !(PRUNE && near[c] > bound);
+      kt[c] = take ? near[c] : INFINITY;
+      kn[c] = take ? ch[c] : -1;
+    }
+#define SRR_CSWAP(a, b)                                          \
+  if (kn[b] >= 0 && (kn[a] < 0 || kt[b] < kt[a])) {              \
+    float tt_ = kt[a]; kt[a] = kt[b]; kt[b] = tt_;               \
+    int nn_ = kn[a]; kn[a] = kn[b]; kn[b] = nn_;                 \
+  }
+    SRR_CSWAP(0, 1) SRR_CSWAP(2, 3) SRR_CSWAP(0, 2) SRR_CSWAP(1, 3) SRR_CSWAP(1, 2)
+#undef SRR_CSWAP
+    if (kn[0] >= 0) {
+      node = kn[0];
+#pragma unroll
+      for (int c = 3; c >= 1; --c) {
+        if (kn[c] < 0) continue;
+        if (sp < kStack) {
+          cx.st_node[sp * kTraceBlock] = kn[c];
+          cx.st_t[sp * kTraceBlock] = kt[c];
+          ++sp;
+        } else {
+          overflow = true;
+        }
+      }
+      continue;
+    }
+    // pop the nearest pending subtree that may still hold a closer hit
+    int nx = -1;
+    while (sp > 0) {
+      --sp;
+      const int cand = cx.st_node[sp * kTraceBlock];
+      if (!(PRUNE && cx.st_t[sp * kTraceBlock] > bound)) { nx = cand; break; }
+    }
+    if (nx < 0) break;
+    node = nx;
+  }
+  if (cx.ctr && !TIMING) {
+    atomicAdd(cx.ctr, (unsigned long long)nbox);
+    atomicAdd(cx.ctr + 1, (unsigned long long)ntri);
+    if (overflow) atomicAdd(cx.ctr + 2, 1ull);
+    // diagnostics: histograms of node steps per ray and per wave (max over lanes)
+    const int steps = (int)(nbox / 4);
+    atomicAdd(cx.ctr + 3 + min(steps, 63), 1ull);
+    int wmax = steps;
+    for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, __shfl_xor(wmax, o));
+    if ((int)__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) atomicAdd(cx.ctr + 67 + min(wmax, 63), 1ull);
+  }
+  if (TIMING) {
+    int st = (int)(nbox / 4);
+    for (int o = 32; o > 0; o >>= 1) st = max(st, __shfl_xor(st, o));
+    cx.mesh_steps += st;
+    cx.mesh_cycles += __builtin_amdgcn_s_memtime() - tm_enter;
+  }
+  if (overflow) return mesh_hit<false>(S, m, r, tmin, tmax, is_medium, out, cx.ctr);  // rare: exact re-walk
   out.t = best_t;
   out.tri = best_i;
   return found;
@@ -181,9 +365,10 @@ SRR_D bool mesh_hit(const SceneView& S, const DMesh& m, const Ray& r, float tmin
 
 // Instance chain (outermost first): the ray going in (hitable.h:44-52, 109-116,
 // 180-188; flip leaves the ray alone)
+template <int TR = 0>
 SRR_D Ray chain_in(const SceneView& S, const DObj& ob, Ray r) {
   for (int k = 0; k < ob.xf_count; ++k) {
-    DXform x = cload(S.xforms, ob.xf_begin + k);
+    DXform x = wload<TR>(S.xforms, ob.xf_begin + k);
     if (x.kind == XF_TRANSLATE) r.o = r.o - v3(x.a, x.b, x.c);
     else if (x.kind == XF_ROTY || x.kind == XF_ROTX) {
       int ia = x.kind == XF_ROTY ? 0 : 1;
@@ -226,19 +411,19 @@ struct ObjHit {
 };
 
 // hit of one non-medium flattened object (in its local frame)
-template <bool PF>
+template <int TR>
 SRR_D bool basic_hit(const SceneView& S, const DObj& ob, const Ray& lr, float tmin, float tmax, bool is_medium,
-                     ObjHit& h, uint32_t* ctr) {
+                     ObjHit& h, const TraceCtx& cx) {
   switch (ob.kind) {
     case OBJ_SPHERE:
     case OBJ_MSPHERE:
-      return sphere_hit(cload(S.spheres, ob.idx), ob.kind == OBJ_MSPHERE, lr, tmin, tmax, h.t);
+      return sphere_hit(wload<TR>(S.spheres, ob.idx), ob.kind == OBJ_MSPHERE, lr, tmin, tmax, h.t);
     case OBJ_RECT: {
       float u, v;
-      return rect_hit(cload(S.rects, ob.idx), lr, tmin, tmax, h.t, u, v);
+      return rect_hit(wload<TR>(S.rects, ob.idx), lr, tmin, tmax, h.t, u, v);
     }
     case OBJ_TRI: {
-      const DStandaloneTri T = cload(S.stris, ob.idx);
+      const DStandaloneTri T = wload<TR>(S.stris, ob.idx);
       V3 p0 = v3(T.p[0], T.p[1], T.p[2]), p1 = v3(T.p[3], T.p[4], T.p[5]), p2 = v3(T.p[6], T.p[7], T.p[8]);
       V3 dir = lr.d / length(lr.d);
       float u, v;
@@ -248,7 +433,11 @@ SRR_D bool basic_hit(const SceneView& S, const DObj& ob, const Ray& lr, float tm
     }
     case OBJ_MESH: {
       MeshHit mh;
-      if (!mesh_hit<PF>(S, cload(S.meshes, ob.idx), lr, tmin, tmax, is_medium, mh, ctr)) return false;
+      const DMesh m = wload<TR>(S.meshes, ob.idx);
+      bool hit;
+      if (tr_mode(TR) == TR_BVH2) hit = mesh_hit<false>(S, m, lr, tmin, tmax, is_medium, mh, cx.ctr);
+      else hit = mesh_hit4<tr_mode(TR) != TR_BVH4, tr_mode(TR) == TR_BVH4_TIMED>(S, m, lr, tmin, tmax, is_medium, mh, cx);
+      if (!hit) return false;
       h.t = mh.t;
       h.prim = mh.tri;
       return true;
@@ -259,15 +448,15 @@ SRR_D bool basic_hit(const SceneView& S, const DObj& ob, const Ray& lr, float tm
 
 // hitable_list::hit (hitable_list.h:21-33) over objects [b, b+n) -- used for a
 // medium's boundary (which sees is_medium = true)
-template <bool PF>
+template <int TR>
 SRR_D bool list_hit(const SceneView& S, int b, int n, const Ray& r, float tmin, float tmax, bool is_medium, float& t,
-                    uint32_t* ctr) {
+                    const TraceCtx& cx) {
   bool any = false;
   float closest = tmax;
   for (int k = 0; k < n; ++k) {
-    const DObj ob = cload(S.objs, b + k);
+    const DObj ob = wload<TR>(S.objs, b + k);
     ObjHit h;
-    if (basic_hit<PF>(S, ob, chain_in(S, ob, r), tmin, closest, is_medium, h, ctr)) {
+    if (basic_hit<TR>(S, ob, chain_in<TR>(S, ob, r), tmin, closest, is_medium, h, cx)) {
       any = true;
       closest = h.t;
       t = h.t;
@@ -277,13 +466,13 @@ SRR_D bool list_hit(const SceneView& S, int b, int n, const Ray& r, float tmin, 
 }
 
 // constant_medium.h:19-50 (two draws, one even on a miss)
-template <bool PF>
+template <int TR>
 SRR_D bool medium_hit(const SceneView& S, const DMedium& md, const Ray& r, float tmin, float tmax, Rng& rng,
-                      float& t, uint32_t* ctr) {
+                      float& t, const TraceCtx& cx) {
   (void)(drand(rng) < 0.00001);
   float t1, t2;
-  if (list_hit<PF>(S, md.bnd_begin, md.bnd_count, r, -FLT_MAX, FLT_MAX, true, t1, ctr)) {
-    if (list_hit<PF>(S, md.bnd_begin, md.bnd_count, r, t1 + 0.0001, FLT_MAX, true, t2, ctr)) {
+  if (list_hit<TR>(S, md.bnd_begin, md.bnd_count, r, -FLT_MAX, FLT_MAX, true, t1, cx)) {
+    if (list_hit<TR>(S, md.bnd_begin, md.bnd_count, r, t1 + 0.0001, FLT_MAX, true, t2, cx)) {
       if (t1 < tmin) t1 = tmin;
       if (t2 > tmax) t2 = tmax;
       if (t1 >= t2) return false;
@@ -308,21 +497,21 @@ struct WorldHit {
   float t;
 };
 
-template <bool MEDIA, bool PF>
-SRR_D WorldHit world_hit(const SceneView& S, const Ray& r, Rng& rng, uint32_t* ctr) {
+template <bool MEDIA, int TR>
+SRR_D WorldHit world_hit(const SceneView& S, const Ray& r, Rng& rng, const TraceCtx& cx) {
   WorldHit w{-1, -1, 0};
   float closest = FLT_MAX;  // numeric_limits<float>::max(), Raytracing_n.cpp:58
   const float tmin = 0.001f;
   for (int k = 0; k < S.n_world; ++k) {
-    const DObj ob = cload(S.objs, k);
-    Ray lr = chain_in(S, ob, r);
+    const DObj ob = wload<TR>(S.objs, k);
+    Ray lr = chain_in<TR>(S, ob, r);
     ObjHit h;
     bool hit;
     if (MEDIA && ob.kind == OBJ_MEDIUM) {
-      hit = medium_hit<PF>(S, cload(S.media, ob.idx), lr, tmin, closest, rng, h.t, ctr);
+      hit = medium_hit<TR>(S, wload<TR>(S.media, ob.idx), lr, tmin, closest, rng, h.t, cx);
       h.prim = -1;
     } else {
-      hit = basic_hit<PF>(S, ob, lr, tmin, closest, false, h, ctr);
+      hit = basic_hit<TR>(S, ob, lr, tmin, closest, false, h, cx);
     }
     if (hit) {
       closest = h.t;
@@ -389,7 +578,7 @@ SRR_D HitRec world_record(const SceneView& S, const Ray& r, const WorldHit& w) {
         p2 = v3(T.p[6], T.p[7], T.p[8]);
         sh = &T.sh;
       } else {
-        const float4* tp = S.tri_pos + 3 * (size_t)w.prim;
+        const float4* tp = S.tri_pos + kTriStride * (size_t)w.prim;
         float4 a = tp[0], b = tp[1], c = tp[2];
         p0 = v3(a.x, a.y, a.z);
         p1 = v3(b.x, b.y, b.z);
@@ -421,6 +610,45 @@ SRR_D HitRec world_record(const SceneView& S, const Ray& r, const WorldHit& w) {
   }
   chain_out(S, ob, h.p, h.n);
   return h;
+}
+
+// Material families for the per-bounce sort: the trace kernel bins every ray
+// into one list per family so each shade kernel carries only its family's
+// code (and registers).  Only diffuse_light emits and it never scatters, so a
+// scattering bounce always has emitted == 0 (material.h:89-92).
+enum Family : int { FAM_TERM = 0, FAM_DIFF = 1, FAM_BECK = 2, FAM_SPEC = 3 };
+
+SRR_D int family_of(int mat, int kind, int depth, int max_depth) {
+  if (mat < 0 || kind == MAT_DIFFUSE_LIGHT || depth >= max_depth) return FAM_TERM;  // Raytracing_n.cpp:63
+  if (kind == MAT_LAMBERTIAN || kind == MAT_ORENNAYAR) return FAM_DIFF;
+  if (kind == MAT_BECKMANN) return FAM_BECK;
+  return FAM_SPEC;
+}
+
+// Material of a world hit without building its record (the trace kernels bin
+// rays by material family with it).
+SRR_D int hit_material(const SceneView& S, const WorldHit& w) {
+  const DObj ob = S.objs[w.obj];
+  switch (ob.kind) {
+    case OBJ_SPHERE:
+    case OBJ_MSPHERE: return S.spheres[ob.idx].mat;
+    case OBJ_RECT: return S.rects[ob.idx].mat;
+    case OBJ_TRI: return S.stris[ob.idx].sh.mat;
+    case OBJ_MESH: return S.tri_shade[w.prim].mat;
+    case OBJ_MEDIUM: return S.media[ob.idx].phase_mat;
+  }
+  return -1;
+}
+
+SRR_D void store_hit(const SceneView& S, const PathState& P, int p, const WorldHit& w, int max_depth, int& fam) {
+  if (w.obj < 0) {
+    nts(&P.hit_w[p], make_int4(-1, -1, 0, -1));
+    fam = FAM_TERM;
+    return;
+  }
+  const int mat = hit_material(S, w);
+  nts(&P.hit_w[p], make_int4(w.obj, w.prim, __float_as_int(w.t), mat));
+  fam = family_of(mat, mat >= 0 ? S.mats[mat].kind : -1, ntl(&P.depth[p]), max_depth);
 }
 
 // ================================================================ shading
@@ -855,6 +1083,22 @@ __device__ __forceinline__ void append(bool pred, int value, int* list, int* cou
   }
 }
 
+// append() for the four material families at once: the four list counters are
+// bumped by one atomic instruction (lanes 0-3), so a wave pays one round trip.
+__device__ __forceinline__ void append4(int fam, int value, int* lists, int list_cap, int* counts) {
+  const uint64_t m0 = __ballot(fam == 0), m1 = __ballot(fam == 1), m2 = __ballot(fam == 2), m3 = __ballot(fam == 3);
+  if ((m0 | m1 | m2 | m3) == 0) return;
+  const int l = lane_id();
+  const uint64_t mine = l == 0 ? m0 : l == 1 ? m1 : l == 2 ? m2 : m3;
+  int base = 0;
+  if (l < 4 && mine) base = atomicAdd(counts + l, __popcll(mine));
+  base = __shfl(base, fam >= 0 ? fam : 0);
+  if (fam >= 0) {
+    const uint64_t m = fam == 0 ? m0 : fam == 1 ? m1 : fam == 2 ? m2 : m3;
+    lists[fam * list_cap + base + __popcll(m & ((1ull << l) - 1))] = value;
+  }
+}
+
 __global__ void __launch_bounds__(256) k_raygen(SceneView S, PathState P, BatchInfo B) {
   int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= B.n_paths) return;
@@ -895,62 +1139,305 @@ __global__ void __launch_bounds__(256) k_raygen(SceneView S, PathState P, BatchI
            v * v3(C.vertical[0], C.vertical[1], C.vertical[2]) - org - offset;
   dir = unit_vector(dir);
   V3 o = org + offset;
-  P.ray_o[p] = make_float4(o.x, o.y, o.z, time);
-  P.ray_d[p] = make_float4(dir.x, dir.y, dir.z, 0.f);
-  P.lcg[p] = rng.lcg;
-  P.pcg[p] = rng.pcg;
-  P.depth[p] = 0;
-  P.spec[p] = 0;
+  nts(&P.ray_o[p], make_float4(o.x, o.y, o.z, time));
+  nts(&P.ray_d[p], make_float4(dir.x, dir.y, dir.z, 0.f));
+  nts(&P.lcg[p], rng.lcg);
+  nts(&P.pcg[p], rng.pcg);
+  nts(&P.depth[p], 0);
+  nts(&P.spec[p], 0);
   B.active[B.act0 + q] = p;
   if (P.rays) P.rays[p] = 0;
 }
 
-// Material families for the per-bounce sort: the trace kernel bins every ray
-// into one list per family so each shade kernel carries only its family's
-// code (and registers).  Only diffuse_light emits and it never scatters, so a
-// scattering bounce always has emitted == 0 (material.h:89-92).
-enum Family : int { FAM_TERM = 0, FAM_DIFF = 1, FAM_BECK = 2, FAM_SPEC = 3 };
 
-SRR_D int family_of(int mat, int kind, int depth, int max_depth) {
-  if (mat < 0 || kind == MAT_DIFFUSE_LIGHT || depth >= max_depth) return FAM_TERM;  // Raytracing_n.cpp:63
-  if (kind == MAT_LAMBERTIAN || kind == MAT_ORENNAYAR) return FAM_DIFF;
-  if (kind == MAT_BECKMANN) return FAM_BECK;
-  return FAM_SPEC;
-}
-
-template <bool MEDIA, bool PF>
-__global__ void __launch_bounds__(256) k_trace(SceneView S, PathState P, const int* active, const int* count,
-                                               int* lists, int list_cap, int* fam_count, int max_depth,
-                                               uint32_t* ctr) {
+template <bool MEDIA, int TR>
+__global__ void __launch_bounds__(kTraceBlock) k_trace(SceneView S0, PathState P, const int* active, const int* count,
+                                                       int* lists, int list_cap, int* fam_count, int max_depth,
+                                                       unsigned long long* ctr) {
+  const uint64_t t_start = tr_mode(TR) == TR_BVH4_TIMED ? __builtin_amdgcn_s_memtime() : 0;
+  SceneView S = S0;
+  if constexpr ((TR & TR_WL) != 0) {  // world tables -> LDS, once per block
+    __shared__ uint4 s_world[kWorldLdsBytes / 16];
+    for (int i = threadIdx.x; i < S0.world_words; i += blockDim.x) s_world[i] = S0.world_blob[i];
+    __syncthreads();
+    const char* b = (const char*)s_world;
+    S.objs = (const DObj*)(b + S0.world_off[0]);
+    S.xforms = (const DXform*)(b + S0.world_off[1]);
+    S.spheres = (const DSphere*)(b + S0.world_off[2]);
+    S.rects = (const DRect*)(b + S0.world_off[3]);
+    S.stris = (const DStandaloneTri*)(b + S0.world_off[4]);
+    S.meshes = (const DMesh*)(b + S0.world_off[5]);
+    S.media = (const DMedium*)(b + S0.world_off[6]);
+  }
+  TraceCtx cx{ctr, nullptr, nullptr};
+  if constexpr (tr_mode(TR) != TR_BVH2) {
+    __shared__ int s_node[kStack * kTraceBlock];
+    __shared__ float s_t[kStack * kTraceBlock];
+    cx.st_node = s_node + threadIdx.x;
+    cx.st_t = s_t + threadIdx.x;
+  }
+  const uint64_t t_staged = tr_mode(TR) == TR_BVH4_TIMED ? __builtin_amdgcn_s_memtime() : 0;
+  uint64_t t_ray = t_staged, t_hit = t_staged;
   int q = blockIdx.x * blockDim.x + threadIdx.x;
   int n = *count;
   int p = -1, fam = -1;
   if (q < n) {
     p = active[q];
-    float4 ro = P.ray_o[p], rdv = P.ray_d[p];
+    float4 ro = ntl(&P.ray_o[p]), rdv = ntl(&P.ray_d[p]);
     Ray r{v3(ro.x, ro.y, ro.z), v3(rdv.x, rdv.y, rdv.z), ro.w};
-    Rng rng{P.lcg[p], P.pcg[p]};
-    WorldHit w = world_hit<MEDIA, PF>(S, r, rng, ctr);
-    if (MEDIA) P.lcg[p] = rng.lcg;
-    if (w.obj < 0) {
-      P.hit_mat[p] = -2;
-      fam = FAM_TERM;
-    } else {
-      HitRec h = world_record(S, r, w);
-      P.hit_p[p] = make_float4(h.p.x, h.p.y, h.p.z, h.u);
-      P.hit_n[p] = make_float4(h.n.x, h.n.y, h.n.z, h.v);
-      P.hit_mat[p] = h.mat;
-      fam = family_of(h.mat, h.mat >= 0 ? S.mats[h.mat].kind : -1, P.depth[p], max_depth);
+    Rng rng{ntl(&P.lcg[p]), ntl(&P.pcg[p])};
+    if (tr_mode(TR) == TR_BVH4_TIMED) {
+      __builtin_amdgcn_s_waitcnt(0);  // diagnostics: ray loaded
+      t_ray = __builtin_amdgcn_s_memtime();
+    }
+    WorldHit w = world_hit<MEDIA, TR>(S, r, rng, cx);
+    if (tr_mode(TR) == TR_BVH4_TIMED) t_hit = __builtin_amdgcn_s_memtime();
+    if (MEDIA) nts(&P.lcg[p], rng.lcg);
+    store_hit(S, P, p, w, max_depth, fam);
+  }
+  append4(fam, p, lists, list_cap, fam_count);
+  if (tr_mode(TR) == TR_BVH4_TIMED && ctr && n >= (1 << 20) && __lane_id() == 0) {  // diagnostics: one record per wave
+    const unsigned long long k = atomicAdd(ctr, 1ull);
+    if (k < kTimingCap) {
+      unsigned long long* e = ctr + 1 + 8 * k;
+      e[0] = __builtin_amdgcn_s_memtime() - t_start;
+      e[1] = cx.mesh_cycles;
+      e[2] = (unsigned long long)cx.mesh_steps;
+      e[3] = t_staged - t_start;
+      e[4] = t_ray - t_staged;
+      e[5] = t_hit - t_ray;
+      e[6] = __builtin_amdgcn_s_memtime() - t_hit;
     }
   }
-  for (int f = 0; f < 4; ++f) append(fam == f, p, lists + f * list_cap, fam_count + f);
+}
+
+// Persistent trace with dynamic ray fetch (scenes without media).  A wave of
+// the per-ray kernel above runs until its longest mesh traversal ends, with the
+// lanes of finished rays idle (~40 % lane utilisation measured); here each lane
+// runs a small state machine -- world objects in list order, then the mesh's
+// node steps, then the hit record -- and lanes whose ray is done fetch the next
+// one from the active list (one wave-aggregated atomic per refill), so the wave
+// keeps its lanes busy until the list is drained.  Same arithmetic, same
+// results as world_hit + world_record.
+constexpr int kMeshSteps = 4;  // node steps per lane between refill checks
+
+template <bool PRUNE>
+__global__ void __launch_bounds__(kTraceBlock) k_trace_pf(SceneView S, PathState P, const int* active,
+                                                          const int* count, int* fetch, int* lists, int list_cap,
+                                                          int* fam_count, int max_depth, unsigned long long* ctr) {
+  const int n = *count;
+  const int n_world = S.n_world;
+  int p = -1;              // path of the lane's ray; -1 idle
+  bool exhausted = false;  // active list drained for this lane
+  Ray r{};
+  int k = 0;               // next world object
+  float closest = FLT_MAX;
+  int wobj = -1, wprim = -1;
+  float wt = 0;
+  // mesh traversal state (threaded BVH2, mesh_hit)
+  bool in_mesh = false;
+  V3 mo{}, md{}, inv{}, dir{};
+  float bound = 0, to_param = 0;
+  int node = 0, end = 0;
+  float4 nlo{}, nhi{};
+  bool found = false;
+  float best_t = 0;
+  int best_i = -1;
+  uint32_t nbox = 0, ntri = 0;
+  for (;;) {
+    // refill idle lanes
+    const bool need = p < 0 && !exhausted;
+    const uint64_t nm = __ballot(need);
+    if (nm) {
+      const int leader = __ffsll((unsigned long long)nm) - 1;
+      int base = 0;
+      if (lane_id() == leader) base = atomicAdd(fetch, __popcll(nm));
+      base = __shfl(base, leader);
+      if (need) {
+        const int idx = base + __popcll(nm & ((1ull << lane_id()) - 1));
+        if (idx < n) {
+          p = active[idx];
+          const float4 ro = ntl(&P.ray_o[p]), rdv = ntl(&P.ray_d[p]);
+          r = Ray{v3(ro.x, ro.y, ro.z), v3(rdv.x, rdv.y, rdv.z), ro.w};
+          k = 0;
+          closest = FLT_MAX;
+          wobj = -1;
+          wprim = -1;
+        } else {
+          exhausted = true;
+        }
+      }
+    }
+    if (__ballot(p >= 0) == 0) break;
+    int fam = -1, fin_p = -1;
+    if (p >= 0) {
+      if (!in_mesh) {
+        // world objects in order (hitable_list::hit) up to the next mesh
+        while (k < n_world) {
+          const DObj ob = S.objs[k];
+          const Ray lr = chain_in(S, ob, r);
+          if (ob.kind == OBJ_MESH) {
+            const DMesh m = S.meshes[ob.idx];
+            mo = lr.o;
+            md = lr.d;
+            inv = v3(1.0f / md.x, 1.0f / md.y, 1.0f / md.z);
+            const float len = length(md);
+            dir = md / len;
+            to_param = kPruneSlack / len;
+            bound = closest;
+            node = m.node_off;
+            end = m.node_off + m.n_nodes;
+            nlo = S.nodes[2 * (node)];
+            nhi = S.nodes[2 * (node) + 1];
+            found = false;
+            best_i = -1;
+            in_mesh = true;
+            break;
+          }
+          ObjHit h;
+          if (basic_hit<TR_BVH2>(S, ob, lr, 0.001f, closest, false, h, TraceCtx{nullptr, nullptr, nullptr})) {
+            closest = h.t;
+            wobj = k;
+            wprim = h.prim;
+            wt = h.t;
+          }
+          ++k;
+        }
+        if (!in_mesh) {  // all objects done: store the winner, bin by material family
+          store_hit(S, P, p, WorldHit{wobj, wprim, wt}, max_depth, fam);
+          fin_p = p;
+          p = -1;
+        }
+      } else {
+        for (int st = 0; st < kMeshSteps; ++st) {
+          ++nbox;
+          const int skip = __float_as_int(nlo.w);
+          const int leaf = __float_as_int(nhi.w);
+          const bool hit = slab(nlo, nhi, mo, inv, 0.001f, bound);
+          if (hit && leaf >= 0) {
+            const int first = leaf >> 1, cnt = (leaf & 1) + 1;
+            ntri += 2;
+            for (int ti = first; ti < first + cnt; ++ti) {
+              const float4* tp = S.tri_pos + kTriStride * (size_t)ti;
+              const float4 a = tp[0], b = tp[1], c = tp[2];
+              float t, u, v;
+              if (tri_hit(v3(a.x, a.y, a.z), v3(b.x, b.y, b.z), v3(c.x, c.y, c.z), true, mo, dir, t, u, v) &&
+                  (!found || wins(t, ti, best_t, best_i))) {
+                found = true;
+                best_t = t;
+                best_i = ti;
+              }
+            }
+            if (PRUNE && found && best_t * to_param < bound) bound = best_t * to_param;
+          }
+          const int next = (hit && leaf < 0) ? node + 1 : skip;
+          if (next >= end) {  // mesh done: it is the list's latest hit if it hit
+            if (found) {
+              closest = best_t;
+              wobj = k;
+              wprim = best_i;
+              wt = best_t;
+            }
+            ++k;
+            in_mesh = false;
+            break;
+          }
+          node = next;
+          nlo = S.nodes[2 * (node)];
+          nhi = S.nodes[2 * (node) + 1];
+        }
+      }
+    }
+    for (int f = 0; f < 4; ++f) append(fam == f, fin_p, lists + f * list_cap, fam_count + f);
+  }
+  if (ctr) {
+    atomicAdd(ctr, (unsigned long long)nbox);
+    atomicAdd(ctr + 1, (unsigned long long)ntri);
+  }
+}
+
+// Hit records of the traced rays (world_record), kept out of the trace kernels
+// so their register budget stays with the traversal.
+__global__ void __launch_bounds__(256) k_record(SceneView S, PathState P, const int* active, const int* count) {
+  const int n = *count;
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
+    const int p = active[q];
+    const int4 hw = ntl(&P.hit_w[p]);
+    if (hw.x < 0 || hw.w < 0) continue;  // miss / null material: no record is read
+    const float4 ro = ntl(&P.ray_o[p]), rdv = ntl(&P.ray_d[p]);
+    const Ray r{v3(ro.x, ro.y, ro.z), v3(rdv.x, rdv.y, rdv.z), ro.w};
+    const HitRec h = world_record(S, r, WorldHit{hw.x, hw.y, __int_as_float(hw.z)});
+    nts(&P.hit_p[p], make_float4(h.p.x, h.p.y, h.p.z, h.u));
+    nts(&P.hit_n[p], make_float4(h.n.x, h.n.y, h.n.z, h.v));
+  }
+}
+
+// Diagnostic probes (SRR_PROBE=1, timing attribution only): the trace kernel's
+// stages re-run over the same active rays with their results discarded.
+// MODE 0: load the ray; 1: + world list without meshes; 4: + mesh instance
+// transform and ray setup; 5: + the mesh's first node; 2: + meshes (the full
+// closest-hit); 3: + hit record.
+template <bool MEDIA, int TR, int MODE>
+__global__ void __launch_bounds__(kTraceBlock) k_probe(SceneView S, PathState P, const int* active, const int* count,
+                                                       int* sink) {
+  TraceCtx cx{nullptr, nullptr, nullptr};
+  if constexpr (TR != TR_BVH2) {
+    __shared__ int s_node[kStack * kTraceBlock];
+    __shared__ float s_t[kStack * kTraceBlock];
+    cx.st_node = s_node + threadIdx.x;
+    cx.st_t = s_t + threadIdx.x;
+  }
+  int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= *count) return;
+  int p = active[q];
+  float4 ro = ntl(&P.ray_o[p]), rdv = ntl(&P.ray_d[p]);
+  Ray r{v3(ro.x, ro.y, ro.z), v3(rdv.x, rdv.y, rdv.z), ro.w};
+  float acc = ro.x + rdv.y;
+  if (MODE >= 1) {
+    Rng rng{ntl(&P.lcg[p]), ntl(&P.pcg[p])};
+    WorldHit w{-1, -1, 0};
+    if (MODE == 1 || MODE == 4 || MODE == 5) {
+      float closest = FLT_MAX;
+      for (int k = 0; k < S.n_world; ++k) {
+        const DObj ob = wload<TR>(S.objs, k);
+        if (ob.kind == OBJ_MEDIUM) continue;
+        if (ob.kind == OBJ_MESH) {
+          if (MODE == 1) continue;
+          const Ray lr = chain_in(S, ob, r);
+          const DMesh m = wload<TR>(S.meshes, ob.idx);
+          const V3 inv = v3(1.0f / lr.d.x, 1.0f / lr.d.y, 1.0f / lr.d.z);
+          const float len = length(lr.d);
+          const V3 dir = lr.d / len;
+          acc += inv.x + inv.y + inv.z + dir.x + dir.y + dir.z + (float)m.node4_off;
+          if (MODE == 5) {  // + the first 4-wide node and its leaf boxes
+            const float4* N = S.node4 + 8 * (size_t)m.node4_off;
+            float4 a = N[0], b = N[3], c = N[6];
+            acc += (a.x - lr.o.x) * inv.x + (b.y - lr.o.y) * inv.y + c.z;
+          }
+          continue;
+        }
+        ObjHit h;
+        if (basic_hit<TR>(S, ob, chain_in(S, ob, r), 0.001f, closest, false, h, cx)) { closest = h.t; w.obj = k; }
+      }
+      acc += closest;
+    } else {
+      w = world_hit<MEDIA, TR>(S, r, rng, cx);
+      acc += w.t;
+      if (MODE == 3 && w.obj >= 0) {
+        HitRec h = world_record(S, r, w);
+        acc += h.p.x + h.n.y + h.u;
+      }
+    }
+    acc += (float)w.obj;
+  }
+  if (acc == 1234.5678f) sink[0] = p;  // keeps the work alive
 }
 
 // Folds the recorded bounces back to front exactly like the recursion returns
 // (Raytracing_n.cpp:69 and :94), then de_nan and store the sample.
 __device__ void finish_path(const PathState& P, int p, V3 C, int depth, uint64_t spec, int max_depth) {
   for (int k = depth - 1; k >= 0; --k) {
-    float4 a = P.rec_a[(size_t)p * max_depth + k];
+    float4 a = ntl(&P.rec_a[(size_t)p * max_depth + k]);
     V3 av = v3(a.x, a.y, a.z);
     if ((spec >> k) & 1) C = av * C;
     else C = v3(0.f) + (av * C) / a.w;  // emitted (== 0) + attenuation*pdf*color / pdf_val
@@ -964,28 +1451,28 @@ __device__ void finish_path(const PathState& P, int p, V3 C, int depth, uint64_t
   if (!(C.x == C.x)) C.x = 0;
   if (!(C.y == C.y)) C.y = 0;
   if (!(C.z == C.z)) C.z = 0;
-  P.sample[3 * (size_t)p] = C.x;
-  P.sample[3 * (size_t)p + 1] = C.y;
-  P.sample[3 * (size_t)p + 2] = C.z;
+  nts(&P.sample[3 * (size_t)p], C.x);
+  nts(&P.sample[3 * (size_t)p + 1], C.y);
+  nts(&P.sample[3 * (size_t)p + 2], C.z);
 }
 
 // One hit of family F (color(), Raytracing_n.cpp:55-106).  Returns true when the
 // path continues with a new ray.
 template <int F>
 SRR_D bool shade_one(const SceneView& S, const PathState& P, int p, int max_depth) {
-  float4 ro = P.ray_o[p], rdv = P.ray_d[p];
+  float4 ro = ntl(&P.ray_o[p]), rdv = ntl(&P.ray_d[p]);
   V3 rdir = v3(rdv.x, rdv.y, rdv.z);
-  int depth = P.depth[p];
-  uint64_t spec = P.spec[p];
+  int depth = ntl(&P.depth[p]);
+  uint64_t spec = ntl(&P.spec[p]);
   if (P.rays) P.rays[p] += 1;
-  int mat = P.hit_mat[p];
+  const int mat = ntl(&P.hit_w[p]).w;
   if (F == FAM_TERM) {
     // miss -> vec3(0.0) (:104); a null material* is UB in the reference: 0 here;
     // no scatter (light) or depth limit -> emitted (:97-100, material.h:348-354)
     V3 emitted = v3(0.f);
     if (mat >= 0) {
       const DMat& M = S.mats[mat];
-      float4 hp = P.hit_p[p], hn = P.hit_n[p];
+      float4 hp = ntl(&P.hit_p[p]), hn = ntl(&P.hit_n[p]);
       V3 nrm = v3(hn.x, hn.y, hn.z);
       if (M.kind == MAT_DIFFUSE_LIGHT && dot(nrm, rdir) < 0.0)
         emitted = tex_value(S, M.tex, hp.w, hn.w, v3(hp.x, hp.y, hp.z));
@@ -993,11 +1480,11 @@ SRR_D bool shade_one(const SceneView& S, const PathState& P, int p, int max_dept
     finish_path(P, p, emitted, depth, spec, max_depth);
     return false;
   }
-  float4 hp = P.hit_p[p], hn = P.hit_n[p];
+  float4 hp = ntl(&P.hit_p[p]), hn = ntl(&P.hit_n[p]);
   V3 hpt = v3(hp.x, hp.y, hp.z), nrm = v3(hn.x, hn.y, hn.z);
   float hu = hp.w, hv = hn.w;
   const DMat M = S.mats[mat];
-  Rng rng{P.lcg[p], P.pcg[p]};
+  Rng rng{ntl(&P.lcg[p]), ntl(&P.pcg[p])};
   V3 ndir;
   float ntime = 0.0f;  // ray(a, b) defaults time to 0 (ray.h:10) for specular rays
   size_t slot = (size_t)p * max_depth + depth;
@@ -1042,7 +1529,7 @@ SRR_D bool shade_one(const SceneView& S, const PathState& P, int p, int max_dept
       ndir = random_in_unit_sphere(rng);
       atten = tex_value(S, M.tex, hu, hv, hpt);
     }
-    P.rec_a[slot] = make_float4(atten.x, atten.y, atten.z, 0.f);
+    nts(&P.rec_a[slot], make_float4(atten.x, atten.y, atten.z, 0.f));
     spec |= (1ull << depth);
   } else {
     // lambertian / orennayar / beckmann: mixture(light, bsdf) (Raytracing_n.cpp:73-94)
@@ -1070,15 +1557,15 @@ SRR_D bool shade_one(const SceneView& S, const PathState& P, int p, int max_dept
     }
     float spdf = scattering_pdf<F == FAM_BECK>(f, nrm, rdir, ndir);
     V3 as = atten * spdf;
-    P.rec_a[slot] = make_float4(as.x, as.y, as.z, pdf_val);
+    nts(&P.rec_a[slot], make_float4(as.x, as.y, as.z, pdf_val));
     ntime = ro.w;
   }
-  P.ray_o[p] = make_float4(hpt.x, hpt.y, hpt.z, ntime);
-  P.ray_d[p] = make_float4(ndir.x, ndir.y, ndir.z, 0.f);
-  P.lcg[p] = rng.lcg;
-  P.pcg[p] = rng.pcg;
-  P.depth[p] = depth + 1;
-  P.spec[p] = spec;
+  nts(&P.ray_o[p], make_float4(hpt.x, hpt.y, hpt.z, ntime));
+  nts(&P.ray_d[p], make_float4(ndir.x, ndir.y, ndir.z, 0.f));
+  nts(&P.lcg[p], rng.lcg);
+  nts(&P.pcg[p], rng.pcg);
+  nts(&P.depth[p], depth + 1);
+  nts(&P.spec[p], spec);
   return true;
 }
 
@@ -1123,9 +1610,9 @@ __global__ void __launch_bounds__(256) k_accumulate(PathState P, BatchInfo B, fl
   float cx = acc[a], cy = acc[a + 1], cz = acc[a + 2];
   for (int s = 0; s < B.spp_batch; ++s) {
     size_t q = 3 * ((size_t)B.slot0 + (size_t)lp * B.spp_batch + s);
-    cx += P.sample[q];
-    cy += P.sample[q + 1];
-    cz += P.sample[q + 2];
+    cx += ntl(&P.sample[q]);
+    cy += ntl(&P.sample[q + 1]);
+    cz += ntl(&P.sample[q + 2]);
   }
   acc[a] = cx;
   acc[a + 1] = cy;
@@ -1147,23 +1634,119 @@ void launch_raygen(const SceneView& S, const PathState& P, const BatchInfo& B, h
   int g = (B.n_paths + 255) / 256;
   hipLaunchKernelGGL(dev::k_raygen, dim3(g), dim3(256), 0, st, S, P, B);
 }
-void launch_trace(const SceneView& S, const PathState& P, const int* active, const int* count, int max_n,
-                  int* lists, int list_cap, int* fam_count, int max_depth, uint32_t* ctr, hipStream_t st) {
-  int g = (max_n + 255) / 256;
-  static const bool pf = [] {
-    const char* e = getenv("SRR_TRACE_PREFETCH");
-    return !(e && e[0] == '0');
-  }();
-#define SRR_LAUNCH_TRACE(M, F)                                                                              \
-  hipLaunchKernelGGL((dev::k_trace<M, F>), dim3(g), dim3(256), 0, st, S, P, active, count, lists, list_cap, \
-                     fam_count, max_depth, ctr)
-  if (S.has_media) {
-    if (pf) SRR_LAUNCH_TRACE(true, true);
-    else SRR_LAUNCH_TRACE(true, false);
-  } else {
-    if (pf) SRR_LAUNCH_TRACE(false, true);
-    else SRR_LAUNCH_TRACE(false, false);
+static unsigned long long* g_timing = nullptr;
+
+void dump_trace_timing() {  // SRR_TRAVERSAL=timed diagnostics
+  if (!g_timing) return;
+  std::vector<unsigned long long> v(1 + 8 * dev::kTimingCap);
+  (void)hipDeviceSynchronize();
+  (void)hipMemcpy(v.data(), g_timing, v.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+  size_t n = std::min<unsigned long long>(v[0], dev::kTimingCap);
+  std::vector<double> tot, mesh, steps, per, stg, ray, hit, tail;
+  for (size_t k = 0; k < n; ++k) {
+    const unsigned long long* e = &v[1 + 8 * k];
+    stg.push_back((double)e[3]);
+    ray.push_back((double)e[4]);
+    hit.push_back((double)e[5]);
+    tail.push_back((double)e[6]);
+    tot.push_back((double)e[0]);
+    mesh.push_back((double)e[1]);
+    steps.push_back((double)e[2]);
+    if (e[2] > 0) per.push_back((double)e[1] / (double)e[2]);
   }
+  auto pct = [](std::vector<double> x, double q) {
+    if (x.empty()) return 0.0;
+    std::sort(x.begin(), x.end());
+    return x[std::min(x.size() - 1, (size_t)(q * x.size()))];
+  };
+  auto mean = [](const std::vector<double>& x) {
+    double a = 0;
+    for (double y : x) a += y;
+    return x.empty() ? 0.0 : a / x.size();
+  };
+  fprintf(stderr, "trace timing: %zu waves (s_memtime ticks)\n", n);
+  for (auto [name, x] : {std::pair<const char*, std::vector<double>*>{"wave total", &tot}, {"mesh", &mesh},
+                         {"mesh steps (wave max)", &steps}, {"ticks per step", &per}, {"LDS staging", &stg},
+                         {"ray load", &ray}, {"world hit", &hit}, {"store+append", &tail}})
+    fprintf(stderr, "  %-22s mean %10.1f  p10 %10.1f  p50 %10.1f  p90 %10.1f  p99 %10.1f\n", name, mean(*x), pct(*x, .1),
+            pct(*x, .5), pct(*x, .9), pct(*x, .99));
+}
+
+void launch_trace(const SceneView& S, const PathState& P, const int* active, const int* count, int max_n,
+                  int* lists, int list_cap, int* fam_count, int* fetch, int max_depth, unsigned long long* ctr,
+                  hipStream_t st) {
+  int g = (max_n + 255) / 256;
+  // SRR_TRAVERSAL: bvh4prune (default) | bvh4 | bvh2 = one ray per thread over the
+  // SAH 4-wide BVH (with / without closest-hit pruning) or the threaded reference
+  // BVH2; pf | pfprune = persistent dynamic-fetch kernel (slower, kept for study);
+  // timed = bvh4prune with per-wave timing records (diagnostics)
+  static const int tr = [] {
+    const char* e = getenv("SRR_TRAVERSAL");
+    if (e && !strcmp(e, "bvh2")) return (int)dev::TR_BVH2;
+    if (e && !strcmp(e, "bvh4")) return (int)dev::TR_BVH4;
+    if (e && !strcmp(e, "bvh4prune")) return (int)dev::TR_BVH4_PRUNE;
+    if (e && !strcmp(e, "timed")) return (int)dev::TR_BVH4_TIMED;
+    if (e && !strcmp(e, "pf")) return 10;
+    if (e && !strcmp(e, "pfprune")) return 11;
+    return (int)dev::TR_BVH4_PRUNE;
+  }();
+  static const int pf_blocks = [] {
+    const char* e = getenv("SRR_PF_BLOCKS");
+    return e ? std::max(1, atoi(e)) : 1024;
+  }();
+  const int grec = std::min(g, 2048);
+  if (tr >= 10 && !S.has_media) {
+    int gb = std::min(g, pf_blocks);
+    if (tr == 11)
+      hipLaunchKernelGGL((dev::k_trace_pf<true>), dim3(gb), dim3(dev::kTraceBlock), 0, st, S, P, active, count, fetch,
+                         lists, list_cap, fam_count, max_depth, ctr);
+    else
+      hipLaunchKernelGGL((dev::k_trace_pf<false>), dim3(gb), dim3(dev::kTraceBlock), 0, st, S, P, active, count,
+                         fetch, lists, list_cap, fam_count, max_depth, ctr);
+    hipLaunchKernelGGL(dev::k_record, dim3(grec), dim3(256), 0, st, S, P, active, count);
+    return;
+  }
+  static unsigned long long* timing = nullptr;
+  if (tr == dev::TR_BVH4_TIMED && !timing) {
+    (void)hipMalloc((void**)&timing, (1 + 8 * dev::kTimingCap) * sizeof(unsigned long long));
+    (void)hipMemset(timing, 0, (1 + 8 * dev::kTimingCap) * sizeof(unsigned long long));
+    g_timing = timing;
+  }
+  unsigned long long* kctr = tr == dev::TR_BVH4_TIMED ? timing : ctr;
+#define SRR_LAUNCH_TRACE(M, T)                                                                        \
+  hipLaunchKernelGGL((dev::k_trace<M, T>), dim3(g), dim3(dev::kTraceBlock), 0, st, S, P, active, count, \
+                     lists, list_cap, fam_count, max_depth, kctr)
+  const bool wl = S.world_words * 16 <= dev::kWorldLdsBytes && !getenv("SRR_NO_WORLD_LDS");
+#define SRR_LAUNCH_TRACE_W(M, T)                  \
+  if (wl) SRR_LAUNCH_TRACE(M, (T) | dev::TR_WL); \
+  else SRR_LAUNCH_TRACE(M, T);
+#define SRR_LAUNCH_TRACE_M(M)                                                 \
+  if (trm == dev::TR_BVH2) { SRR_LAUNCH_TRACE_W(M, dev::TR_BVH2) }            \
+  else if (trm == dev::TR_BVH4) { SRR_LAUNCH_TRACE_W(M, dev::TR_BVH4) }       \
+  else if (trm == dev::TR_BVH4_TIMED) { SRR_LAUNCH_TRACE_W(M, dev::TR_BVH4_TIMED) } \
+  else { SRR_LAUNCH_TRACE_W(M, dev::TR_BVH4_PRUNE) }
+  const int trm = tr >= 10 ? (int)dev::TR_BVH4_PRUNE : tr;  // media scenes: one ray per thread
+  if (S.has_media) {
+    SRR_LAUNCH_TRACE_M(true)
+  } else {
+    SRR_LAUNCH_TRACE_M(false)
+  }
+  hipLaunchKernelGGL(dev::k_record, dim3(grec), dim3(256), 0, st, S, P, active, count);
+  static const bool probe = getenv("SRR_PROBE") && getenv("SRR_PROBE")[0] == '1';
+  if (probe && !S.has_media) {
+    static int* sink = nullptr;
+    if (!sink) (void)hipMalloc((void**)&sink, 16);
+#define SRR_PROBE(T, M) \
+  hipLaunchKernelGGL((dev::k_probe<false, T, M>), dim3(g), dim3(dev::kTraceBlock), 0, st, S, P, active, count, sink)
+#define SRR_PROBES(T) SRR_PROBE(T, 0); SRR_PROBE(T, 1); SRR_PROBE(T, 4); SRR_PROBE(T, 5); SRR_PROBE(T, 2);
+    if (trm == dev::TR_BVH2) { SRR_PROBES(dev::TR_BVH2) }
+    else if (trm == dev::TR_BVH4) { SRR_PROBES(dev::TR_BVH4) }
+    else { SRR_PROBES(dev::TR_BVH4_PRUNE) }
+#undef SRR_PROBES
+#undef SRR_PROBE
+  }
+#undef SRR_LAUNCH_TRACE_M
+#undef SRR_LAUNCH_TRACE_W
 #undef SRR_LAUNCH_TRACE
 }
 void launch_shade(const SceneView& S, const PathState& P, const int* lists, int list_cap, const int* fam_count,

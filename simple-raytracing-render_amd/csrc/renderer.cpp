@@ -7,8 +7,11 @@
 #include <cstring>
 #include <memory>
 #include <thread>
+#include <cstdio>
 
 namespace srr {
+
+constexpr int kVisitWords = 3 + 2 * 64;  // SRR_FLAG_COUNT_VISITS: sums + two histograms
 
 #define RCHK(x)                                                        \
   do {                                                                 \
@@ -38,7 +41,7 @@ int renderer_create(const Scene& sc, int device, srr_renderer** out, std::string
   if (const char* e = getenv("SRR_LANES")) r->n_lanes = std::max(1, std::min(kMaxLanes, atoi(e)));
   RCHK(hipSetDevice(device));
   std::vector<void*>& K = r->scene_bufs;
-  DObj* objs; DXform* xf; DSphere* sph; DRect* rct; DStandaloneTri* st; DMesh* me; float* nlo; float* nhi;
+  DObj* objs; DXform* xf; DSphere* sph; DRect* rct; DStandaloneTri* st; DMesh* me; float* nodes; float* n4;
   float* tp; TriShade* ts; DMedium* md; DMat* mt; DTex* tx; uint8_t* im; float* pr; int32_t* pp; DLight* li;
   DCamera* cm;
   std::vector<DCamera> cam{F.cam};
@@ -48,8 +51,8 @@ int renderer_create(const Scene& sc, int device, srr_renderer** out, std::string
   RCHK(upload(&rct, F.rects, K));
   RCHK(upload(&st, F.stris, K));
   RCHK(upload(&me, F.meshes, K));
-  RCHK(upload(&nlo, F.node_lo, K));
-  RCHK(upload(&nhi, F.node_hi, K));
+  RCHK(upload(&nodes, F.nodes, K));
+  RCHK(upload(&n4, F.node4, K));
   RCHK(upload(&tp, F.tri_pos, K));
   RCHK(upload(&ts, F.tri_shade, K));
   RCHK(upload(&md, F.media, K));
@@ -60,7 +63,27 @@ int renderer_create(const Scene& sc, int device, srr_renderer** out, std::string
   RCHK(upload(&pp, F.perlin_perm, K));
   RCHK(upload(&li, F.lights, K));
   RCHK(upload(&cm, cam, K));
+  // world-traversal tables packed for LDS staging (kernels.h SceneView::world_blob)
+  std::vector<uint8_t> blob;
+  int off[7];
+  auto put = [&](int k, const void* data, size_t bytes) {
+    off[k] = (int)blob.size();
+    blob.insert(blob.end(), (const uint8_t*)data, (const uint8_t*)data + bytes);
+    blob.resize((blob.size() + 15) & ~(size_t)15, 0);
+  };
+  put(0, F.objs.data(), F.objs.size() * sizeof(DObj));
+  put(1, F.xforms.data(), F.xforms.size() * sizeof(DXform));
+  put(2, F.spheres.data(), F.spheres.size() * sizeof(DSphere));
+  put(3, F.rects.data(), F.rects.size() * sizeof(DRect));
+  put(4, F.stris.data(), F.stris.size() * sizeof(DStandaloneTri));
+  put(5, F.meshes.data(), F.meshes.size() * sizeof(DMesh));
+  put(6, F.media.data(), F.media.size() * sizeof(DMedium));
+  uint8_t* wb;
+  RCHK(upload(&wb, blob, K));
   SceneView& V = r->view;
+  V.world_blob = (const uint4*)wb;
+  V.world_words = (int)(blob.size() / 16);
+  for (int k = 0; k < 7; ++k) V.world_off[k] = off[k];
   V.objs = objs;
   V.n_world = F.n_world;
   V.has_media = F.media.empty() ? 0 : 1;
@@ -69,8 +92,8 @@ int renderer_create(const Scene& sc, int device, srr_renderer** out, std::string
   V.rects = rct;
   V.stris = st;
   V.meshes = me;
-  V.node_lo = (const float4*)nlo;
-  V.node_hi = (const float4*)nhi;
+  V.nodes = (const float4*)nodes;
+  V.node4 = (const float4*)n4;
   V.tri_pos = (const float4*)tp;
   V.tri_shade = ts;
   V.media = md;
@@ -130,9 +153,9 @@ static int ensure_lane(Lane& L, size_t n, int depth, bool keep, std::string& err
   RCHK(lane_alloc(L, &P.pcg, n));
   RCHK(lane_alloc(L, &P.depth, n));
   RCHK(lane_alloc(L, &P.spec, n));
+  RCHK(lane_alloc(L, &P.hit_w, n));
   RCHK(lane_alloc(L, &P.hit_p, n));
   RCHK(lane_alloc(L, &P.hit_n, n));
-  RCHK(lane_alloc(L, &P.hit_mat, n));
   RCHK(lane_alloc(L, &P.rec_a, n * d));
   RCHK(lane_alloc(L, &P.sample, 3 * n));
   RCHK(lane_alloc(L, &L.lists, 4 * n));
@@ -154,6 +177,12 @@ int render_device(srr_renderer* r, const srr_params* p, const int32_t* pix, int6
   const bool keep = (p->flags & SRR_FLAG_KEEP_PATHS) != 0;
   const int R = kRegionsPerLane;
   hipStream_t ast = r->acc_st;
+  unsigned long long* visits = nullptr;
+  if (p->flags & SRR_FLAG_COUNT_VISITS) {
+    if (!r->visits) RCHK(hipMalloc((void**)&r->visits, kVisitWords * sizeof(unsigned long long)));
+    RCHK(hipMemset(r->visits, 0, kVisitWords * sizeof(unsigned long long)));
+    visits = r->visits;
+  }
   // frame buffers
   if ((size_t)npix > r->pix_cap) {
     (void)hipFree(r->pixels);
@@ -304,9 +333,10 @@ int render_device(srr_renderer* r, const srr_params* p, const int32_t* pix, int6
         int* alive = L.cnt + 2;
         int* fam = alive + R;
         RCHK(hipMemsetAsync(L.cnt + (cur ^ 1), 0, sizeof(int), L.st));
-        RCHK(hipMemsetAsync(alive, 0, (R + 4) * sizeof(int), L.st));
+        int* fetch = alive + R + 4;  // persistent trace's ray cursor
+        RCHK(hipMemsetAsync(alive, 0, (R + 5) * sizeof(int), L.st));
         RCHK(hipEventRecord(L.ev_t0, L.st));
-        launch_trace(r->view, L.P, L.act[cur], L.cnt + cur, n, L.lists, (int)L.cap, fam, p->max_depth, nullptr,
+        launch_trace(r->view, L.P, L.act[cur], L.cnt + cur, n, L.lists, (int)L.cap, fam, fetch, p->max_depth, visits,
                      L.st);
         RCHK(hipEventRecord(L.ev_t1, L.st));
         launch_shade(r->view, L.P, L.lists, (int)L.cap, fam, L.act[cur ^ 1], L.cnt + (cur ^ 1), alive, (int)region,
@@ -357,6 +387,23 @@ int render_device(srr_renderer* r, const srr_params* p, const int32_t* pix, int6
     s.trace_ms += r->lanes[l].trace_ms;
     s.shade_ms += r->lanes[l].shade_ms;
   }
+  if (getenv("SRR_TIMING")) dump_trace_timing();
+  if (visits) {
+    unsigned long long v[kVisitWords];
+    RCHK(hipDeviceSynchronize());
+    RCHK(hipMemcpy(v, visits, sizeof(v), hipMemcpyDeviceToHost));
+    if (getenv("SRR_HIST")) {  // diagnostics: node steps per ray / per wave
+      for (int h = 0; h < 2; ++h) {
+        fprintf(stderr, h ? "steps per wave (max):" : "steps per ray:");
+        for (int b = 0; b < 64; ++b)
+          if (v[3 + 64 * h + b]) fprintf(stderr, " %d:%llu", b, v[3 + 64 * h + b]);
+        fprintf(stderr, "\n");
+      }
+    }
+    s.box_tests = (int64_t)v[0];
+    s.tri_tests = (int64_t)v[1];
+    s.stack_overflows = (int64_t)v[2];
+  }
   if (stats) *stats = s;
   return 0;
 }
@@ -367,6 +414,7 @@ srr_renderer::~srr_renderer() {
   (void)hipSetDevice(device);
   (void)hipDeviceSynchronize();
   for (void* p : scene_bufs) (void)hipFree(p);
+  if (visits) (void)hipFree(visits);
   for (auto& L : lanes) {
     srr::free_lane_paths(L);
     (void)hipFree(L.cnt);

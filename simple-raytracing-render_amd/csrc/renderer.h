@@ -58,6 +58,7 @@ struct srr_renderer {
   hipEvent_t ev_beg = nullptr, ev_end = nullptr;
   // frame buffers
   float* acc = nullptr;
+  unsigned long long* visits = nullptr;  // SRR_FLAG_COUNT_VISITS counters (3)
   int32_t* pixels = nullptr;
   size_t pix_cap = 0;
   double* sobol = nullptr;

@@ -5,6 +5,7 @@
 // are bit-identical to the reference's.
 #include "scene.h"
 
+#include <algorithm>
 #include <cfloat>
 #include <cmath>
 #include <cstdlib>
@@ -600,6 +601,164 @@ struct Flattener {
     F.stris.push_back(d);
     return (int)F.stris.size() - 1;
   }
+  // 4-wide BVH for near-first traversal with closest-hit pruning (kernels.hip
+  // mesh_hit4).  The reference's result over a mesh depends only on which of its
+  // LEAF boxes (1-2 triangles each, bvh.h:104-110) the ray's slab test passes:
+  // every ancestor box contains its leaves, so an ancestor passes whenever a leaf
+  // does.  Any hierarchy over the reference's exact leaf boxes therefore reaches
+  // the same leaves.  By default the hierarchy is rebuilt with a binned SAH over
+  // the leaf units (the reference splits at the median of a random axis, which
+  // leaves loose, overlapping boxes); SRR_BVH4=ref collapses the reference
+  // topology instead.  Leaf slots hold the reference's leaf box unchanged; inner
+  // boxes are exact unions of their children.
+  struct TNode {
+    Box3 box;
+    int left = -1, right = -1;
+    int code = -1;  // leaf unit: (first triangle << 1) | (count - 1)
+  };
+  static float box_area(const Box3& b) {
+    float dx = b.mx[0] - b.mn[0], dy = b.mx[1] - b.mn[1], dz = b.mx[2] - b.mn[2];
+    return dx * dy + dy * dz + dz * dx;
+  }
+  static Box3 box_union(const Box3& a, const Box3& b) {
+    Box3 r;
+    for (int k = 0; k < 3; ++k) {
+      r.mn[k] = std::min(a.mn[k], b.mn[k]);
+      r.mx[k] = std::max(a.mx[k], b.mx[k]);
+    }
+    return r;
+  }
+  static std::vector<TNode> tree_from_reference(const HBvh& B, int tri_off) {
+    std::vector<TNode> T(B.nodes.size());
+    for (size_t i = 0; i < B.nodes.size(); ++i) {
+      const HBvh::Node& n = B.nodes[i];
+      T[i].box = n.box;
+      if (n.left < 0) {
+        int first = ~n.left, last = ~n.right;
+        T[i].code = ((first + tri_off) << 1) | (last != first ? 1 : 0);
+      } else {
+        T[i].left = n.left;
+        T[i].right = n.right;
+      }
+    }
+    return T;
+  }
+  static std::vector<TNode> tree_sah(const HBvh& B, int tri_off) {
+    std::vector<TNode> units;
+    for (const HBvh::Node& n : B.nodes)
+      if (n.left < 0) {
+        TNode u;
+        u.box = n.box;
+        int first = ~n.left, last = ~n.right;
+        u.code = ((first + tri_off) << 1) | (last != first ? 1 : 0);
+        units.push_back(u);
+      }
+    std::vector<TNode> T;
+    T.reserve(2 * units.size());
+    auto centroid = [](const TNode& u, int a) { return 0.5f * (u.box.mn[a] + u.box.mx[a]); };
+    std::function<int(int, int)> build = [&](int lo, int hi) -> int {
+      const int me = (int)T.size();
+      T.push_back(TNode{});
+      if (hi - lo == 1) {
+        T[me] = units[lo];
+        return me;
+      }
+      Box3 box = units[lo].box, cb;
+      for (int a = 0; a < 3; ++a) cb.mn[a] = cb.mx[a] = centroid(units[lo], a);
+      for (int i = lo; i < hi; ++i) {
+        box = box_union(box, units[i].box);
+        for (int a = 0; a < 3; ++a) {
+          cb.mn[a] = std::min(cb.mn[a], centroid(units[i], a));
+          cb.mx[a] = std::max(cb.mx[a], centroid(units[i], a));
+        }
+      }
+      constexpr int kBins = 16;
+      int best_axis = -1, best_bin = -1;
+      float best_cost = INFINITY;
+      for (int a = 0; a < 3; ++a) {
+        const float ext = cb.mx[a] - cb.mn[a];
+        if (!(ext > 0.f)) continue;
+        Box3 bb[kBins];
+        int bn[kBins] = {0};
+        for (int i = lo; i < hi; ++i) {
+          int b = std::min(kBins - 1, (int)(kBins * (centroid(units[i], a) - cb.mn[a]) / ext));
+          bb[b] = bn[b] ? box_union(bb[b], units[i].box) : units[i].box;
+          ++bn[b];
+        }
+        for (int s = 0; s < kBins - 1; ++s) {  // split after bin s
+          Box3 L{}, R{};
+          int nl = 0, nr = 0;
+          for (int b = 0; b <= s; ++b)
+            if (bn[b]) { L = nl ? box_union(L, bb[b]) : bb[b]; nl += bn[b]; }
+          for (int b = s + 1; b < kBins; ++b)
+            if (bn[b]) { R = nr ? box_union(R, bb[b]) : bb[b]; nr += bn[b]; }
+          if (!nl || !nr) continue;
+          float cost = box_area(L) * nl + box_area(R) * nr;
+          if (cost < best_cost) { best_cost = cost; best_axis = a; best_bin = s; }
+        }
+      }
+      int mid;
+      if (best_axis >= 0) {
+        const int a = best_axis;
+        const float ext = cb.mx[a] - cb.mn[a];
+        auto it = std::partition(units.begin() + lo, units.begin() + hi, [&](const TNode& u) {
+          return std::min(kBins - 1, (int)(kBins * (centroid(u, a) - cb.mn[a]) / ext)) <= best_bin;
+        });
+        mid = (int)(it - units.begin());
+      } else {
+        mid = (lo + hi) / 2;  // coincident centroids
+      }
+      if (mid <= lo || mid >= hi) mid = (lo + hi) / 2;
+      const int l = build(lo, mid);
+      const int r = build(mid, hi);
+      T[me].box = box;
+      T[me].left = l;
+      T[me].right = r;
+      return me;
+    };
+    build(0, (int)units.size());
+    return T;
+  }
+  void build_node4(const HBvh& B, DMesh& m) {
+    static const bool ref_topology = [] {
+      const char* e = getenv("SRR_BVH4");
+      return e && !strcmp(e, "ref");
+    }();
+    const std::vector<TNode> T = ref_topology ? tree_from_reference(B, m.tri_off) : tree_sah(B, m.tri_off);
+    m.node4_off = (int)(F.node4.size() / 32);
+    std::function<int(int)> build = [&](int top) -> int {
+      std::vector<int> kids{top};
+      while (kids.size() < 4) {  // open the largest inner node until 4 children
+        int best = -1;
+        float ba = -1.f;
+        for (size_t k = 0; k < kids.size(); ++k)
+          if (T[kids[k]].code < 0 && box_area(T[kids[k]].box) > ba) { ba = box_area(T[kids[k]].box); best = (int)k; }
+        if (best < 0) break;
+        const TNode n = T[kids[best]];
+        kids[best] = n.left;
+        kids.insert(kids.begin() + best + 1, n.right);
+      }
+      const int me = (int)(F.node4.size() / 32);
+      F.node4.resize(F.node4.size() + 32);
+      int32_t child[4] = {INT32_MIN, INT32_MIN, INT32_MIN, INT32_MIN};  // empty: never descended
+      float lo[3][4], hi[3][4];
+      for (int c = 0; c < 4; ++c) {
+        for (int a = 0; a < 3; ++a) { lo[a][c] = INFINITY; hi[a][c] = -INFINITY; }  // empty slot
+        if (c >= (int)kids.size()) continue;
+        const TNode& n = T[kids[c]];
+        for (int a = 0; a < 3; ++a) { lo[a][c] = n.box.mn[a]; hi[a][c] = n.box.mx[a]; }
+        child[c] = n.code >= 0 ? ~n.code : build(kids[c]);
+      }
+      float* d = &F.node4[32 * (size_t)me];
+      for (int a = 0; a < 3; ++a)
+        for (int c = 0; c < 4; ++c) { d[4 * a + c] = lo[a][c]; d[12 + 4 * a + c] = hi[a][c]; }
+      std::memcpy(d + 24, child, 16);
+      return me;
+    };
+    build(0);
+    m.n_node4 = (int)(F.node4.size() / 32) - m.node4_off;
+  }
+
   int add_mesh(int h) {  // a bvh_node whose leaves are all bare triangles
     auto it = mesh_of_bvh.find(h);
     if (it != mesh_of_bvh.end()) return it->second;
@@ -607,7 +766,7 @@ struct Flattener {
     for (int l : B.leaves)
       if (S.obj[l].kind != H_TRI) return -1;
     DMesh m{};
-    m.node_off = (int)(F.node_lo.size() / 4);
+    m.node_off = (int)(F.nodes.size() / 8);
     m.tri_off = (int)(F.tri_shade.size());
     m.n_nodes = (int)B.nodes.size();
     m.n_tris = (int)B.leaves.size();
@@ -629,12 +788,13 @@ struct Flattener {
       float sf, lf;
       std::memcpy(&sf, &skip, 4);
       std::memcpy(&lf, &leaf, 4);
-      F.node_lo.insert(F.node_lo.end(), {n.box.mn[0], n.box.mn[1], n.box.mn[2], sf});
-      F.node_hi.insert(F.node_hi.end(), {n.box.mx[0], n.box.mx[1], n.box.mx[2], lf});
+      F.nodes.insert(F.nodes.end(), {n.box.mn[0], n.box.mn[1], n.box.mn[2], sf, n.box.mx[0], n.box.mx[1], n.box.mx[2], lf});
     }
+    build_node4(B, m);
     for (int l : B.leaves) {
       const HTri& t = S.tris[S.obj[l].tri];
       for (int k = 0; k < 3; ++k) F.tri_pos.insert(F.tri_pos.end(), {t.p[3 * k], t.p[3 * k + 1], t.p[3 * k + 2], 0.f});
+      F.tri_pos.insert(F.tri_pos.end(), {0.f, 0.f, 0.f, 0.f});  // pad to one 64-B line
       TriShade sh{};
       std::memcpy(sh.n, t.n, 36);
       for (int k = 0; k < 3; ++k) { sh.uv[2 * k] = t.uv[3 * k]; sh.uv[2 * k + 1] = t.uv[3 * k + 1]; }

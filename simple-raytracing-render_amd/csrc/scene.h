@@ -124,8 +124,9 @@ struct Flat {
   std::vector<DRect> rects;
   std::vector<DStandaloneTri> stris;
   std::vector<DMesh> meshes;
-  std::vector<float> node_lo, node_hi;  // float4 per node
-  std::vector<float> tri_pos;           // float4 x3 per triangle
+  std::vector<float> nodes;             // 2 float4 per node (lo, hi)
+  std::vector<float> node4;             // 8 float4 per 4-wide node
+  std::vector<float> tri_pos;           // float4 x4 per triangle (p0, p1, p2, pad)
   std::vector<TriShade> tri_shade;
   std::vector<DMedium> media;
   std::vector<DMat> mats;

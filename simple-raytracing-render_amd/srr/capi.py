@@ -15,6 +15,7 @@ _LIB = None
 
 FLAG_SORT_MATERIALS = 1
 FLAG_KEEP_PATHS = 2
+FLAG_COUNT_VISITS = 4
 
 
 class SrrError(RuntimeError):
@@ -31,7 +32,8 @@ class Params(ctypes.Structure):
 class Stats(ctypes.Structure):
     _fields_ = [("world_rays", ctypes.c_int64), ("paths", ctypes.c_int64), ("trace_launches", ctypes.c_int64),
                 ("trace_ms", ctypes.c_double), ("shade_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
-                ("bounces", ctypes.c_int64)]
+                ("bounces", ctypes.c_int64), ("box_tests", ctypes.c_int64), ("tri_tests", ctypes.c_int64),
+                ("stack_overflows", ctypes.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

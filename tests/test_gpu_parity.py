@@ -95,6 +95,39 @@ def test_larger_renders_match_oracle_on_sampled_pixels(factory, nx, ny, spp):
     assert pc["match"] >= parity.MIN_MATCH, pc
 
 
+def _nan_panel_scene():
+    """Cornell box + a BVH'd panel of 128 triangles, half of them with zero vertex
+    normals: their shading normal is NaN (unit_vector of 0), so rays scattered off
+    them have NaN directions and pass every slab test (as in the reference)."""
+    from srr.scene import Scene
+    sc = Scene()
+    objs, white = scenes._cornell(sc)
+    tris = []
+    for a in range(8):
+        for b in range(8):
+            x0, x1 = 120 + 40 * a, 160 + 40 * a
+            y0, y1 = 100 + 40 * b, 140 + 40 * b
+            z0, z1 = 250 + 5 * a, 260 + 5 * b
+            n = ((0, 0, 0),) * 3 if (a + b) % 2 == 0 else ((0, 0, -1),) * 3
+            tris.append(sc.triangle((x0, y0, z0), (x1, y0, z1), (x1, y1, z0), white, normals=n))
+            tris.append(sc.triangle((x0, y0, z0), (x1, y1, z0), (x0, y1, z1), white, normals=n))
+    objs.append(sc.bvh_node(tris, 0, 1))
+    sc.set_world(sc.hitable_list(objs))
+    scenes._cornell_camera_and_lights(sc)
+    return sc
+
+
+def test_nan_rays_through_meshes_match_oracle():
+    text = _nan_panel_scene().text()
+    nx, ny, spp = 24, 24, 8
+    out = capi.Renderer(text).render(nx, ny, spp, 50, keep_paths=True)
+    ref = ob.render(text, nx, ny, spp, 50, threads=8)
+    pc = parity.compare_paths(out["paths"], ref["paths"])
+    print("nan panel:", pc, out["stats"]["world_rays"], int(ref["stats"][0]))
+    assert pc["match"] >= parity.MIN_MATCH, pc
+    assert abs(out["stats"]["world_rays"] - int(ref["stats"][0])) <= 0.01 * int(ref["stats"][0])
+
+
 def test_depth_limit_zero_and_one():
     """maxDepth edge cases (Raytracing_n.cpp:63): depth 0 returns emitted only."""
     sc, _ = scenes.s1_cornell()
