@@ -71,7 +71,33 @@ struct BatchInfo {
   uint64_t base_seed;
 };
 
+// One window of a frame for the path-resident persistent kernel (k_paths):
+// every (pixel, sample) of pixels x [0, spp_w) is a path, numbered
+// g = lp * spp_w + s; lanes fetch g from `cursor` as their paths finish.
+struct PathWork {
+  const int32_t* pixels;  // shard pixel list (PPM-order indices), nullptr = identity
+  const double* sobol;    // [spp_w][2], window sample 0 first
+  int npix, spp_w;
+  int s_base;             // global sample index of window sample 0 (per-path seeds)
+  int nx, ny;
+  uint64_t base_seed;
+  int64_t n_paths;        // npix * spp_w
+  int max_depth;
+  unsigned long long* cursor;  // next path to start (device, zeroed per window)
+  unsigned long long* counters;  // [0] += world rays traced
+  float* sample;          // [n_paths][3] de_nan'd radiance
+  float* raw;             // optional [n_paths][3] radiance before de_nan
+  uint8_t* rays;          // optional [n_paths] world rays per path
+  float4* rec;            // bounce records [max_depth][lanes]
+  int lanes;              // persistent lanes (grid * block)
+  int* err;               // guard bits set on an out-of-range index (never expected)
+};
+
+constexpr int kPathsWorldLdsBytes = 8192;  // == kernels.hip kWorldLdsBytes
 void dump_trace_timing();
+int paths_lanes_per_device(const SceneView& S, int device);  // persistent grid capacity
+void launch_paths(const SceneView& S, const PathWork& W, int all_families, hipStream_t st);
+void launch_accumulate_window(const float* sample, int npix, int spp_w, float* acc, hipStream_t st);
 void launch_raygen(const SceneView& S, const PathState& P, const BatchInfo& B, hipStream_t st);
 void launch_trace(const SceneView& S, const PathState& P, const int* active, const int* count, int max_n,
                   int* lists, int list_cap, int* fam_count, int* fetch, int max_depth, unsigned long long* ctr,

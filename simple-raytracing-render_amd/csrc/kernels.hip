@@ -208,7 +208,7 @@ SRR_D T wload(const T* p, int i) {
 }
 constexpr int kTraceBlock = 256;
 constexpr int kStack = 12;
-constexpr int kWorldLdsBytes = 8192;  // world tables staged in LDS up to this size
+constexpr int kWorldLdsBytes = kPathsWorldLdsBytes;  // world tables staged in LDS up to this size
 constexpr unsigned long long kTimingCap = 1 << 16;  // SRR_TIMING wave records  // LDS stack entries per ray; deeper -> exact BVH2 re-walk
 
 struct TraceCtx {
@@ -539,9 +539,10 @@ SRR_D void sphere_uv(V3 p, float& u, float& v) {  // hitable.h:10-15
   v = (theta + kPi / 2) / kPi;
 }
 
+template <int TR = 0>  // TR & TR_WL: world tables in LDS (plain loads, never cload)
 SRR_D HitRec world_record(const SceneView& S, const Ray& r, const WorldHit& w) {
   const DObj& ob = S.objs[w.obj];
-  Ray lr = chain_in(S, ob, r);
+  Ray lr = chain_in<TR>(S, ob, r);
   HitRec h;
   h.u = 0;  // moving_sphere / constant_medium leave u, v unset in the reference;
   h.v = 0;  // defined here as 0
@@ -1099,30 +1100,23 @@ __device__ __forceinline__ void append4(int fam, int value, int* lists, int list
   }
 }
 
-__global__ void __launch_bounds__(256) k_raygen(SceneView S, PathState P, BatchInfo B) {
-  int q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= B.n_paths) return;
-  int lp = q / B.spp_batch;
-  int s = B.s0 + q % B.spp_batch;
-  int p = B.slot0 + q;
-  if (q == 0) *B.count = B.act0 + B.n_paths;
-  int pix = B.pixels[B.p0 + lp];
-  int i = pix % B.nx;
-  int j = B.ny - 1 - pix / B.nx;  // Raytracing_n.cpp:827-828 (SURVEY Q12 fix)
-  // per-path seeding
-  uint64_t h = 0xcbf29ce484222325ULL ^ B.base_seed;
-  uint32_t w[3] = {(uint32_t)i, (uint32_t)j, (uint32_t)(B.s_base + s)};
+// The camera ray of sample s_global of pixel `pix` with its per-path RNG streams
+// (SURVEY §8(d) seeding; Raytracing_n.cpp:827-836; camera::get_ray, camera.h:51-59).
+SRR_D void camera_ray(const SceneView& S, int pix, int s_global, double sx, double sy, int nx, int ny,
+                      uint64_t base_seed, V3& o, V3& dir, float& time, Rng& rng) {
+  int i = pix % nx;
+  int j = ny - 1 - pix / nx;  // Raytracing_n.cpp:827-828 (SURVEY Q12 fix)
+  uint64_t h = 0xcbf29ce484222325ULL ^ base_seed;
+  uint32_t w[3] = {(uint32_t)i, (uint32_t)j, (uint32_t)s_global};
   for (int k = 0; k < 3; ++k)
     for (int b = 0; b < 4; ++b) {
       h ^= (w[k] >> (8 * b)) & 0xffu;
       h *= 0x100000001b3ULL;
     }
-  Rng rng;
   rng.lcg = h & 0xFFFFFFFFFFFFULL;
   rng.pcg = 0x853c49e6748fea9bULL ^ (rng.lcg << 16);
-  // Raytracing_n.cpp:834-836 and camera::get_ray (camera.h:51-59)
-  float u = float(B.sobol[2 * s] + i) / float(B.nx);
-  float v = float(B.sobol[2 * s + 1] + j) / float(B.ny);
+  float u = float(sx + i) / float(nx);
+  float v = float(sy + j) / float(ny);
   const DCamera& C = *S.cam;
   V3 pd;
   do {  // random_in_unit_disk (camera.h:8-14): y drawn before x
@@ -1133,12 +1127,26 @@ __global__ void __launch_bounds__(256) k_raygen(SceneView S, PathState P, BatchI
   V3 rd = C.lens_radius * pd;
   V3 cu = v3(C.u[0], C.u[1], C.u[2]), cv = v3(C.v[0], C.v[1], C.v[2]);
   V3 offset = cu * rd.x + cv * rd.y;
-  float time = C.time0 + drand(rng) * (C.time1 - C.time0);
+  time = C.time0 + drand(rng) * (C.time1 - C.time0);
   V3 org = v3(C.origin[0], C.origin[1], C.origin[2]);
-  V3 dir = v3(C.llc[0], C.llc[1], C.llc[2]) + u * v3(C.horizontal[0], C.horizontal[1], C.horizontal[2]) +
-           v * v3(C.vertical[0], C.vertical[1], C.vertical[2]) - org - offset;
+  dir = v3(C.llc[0], C.llc[1], C.llc[2]) + u * v3(C.horizontal[0], C.horizontal[1], C.horizontal[2]) +
+        v * v3(C.vertical[0], C.vertical[1], C.vertical[2]) - org - offset;
   dir = unit_vector(dir);
-  V3 o = org + offset;
+  o = org + offset;
+}
+
+__global__ void __launch_bounds__(256) k_raygen(SceneView S, PathState P, BatchInfo B) {
+  int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= B.n_paths) return;
+  int lp = q / B.spp_batch;
+  int s = B.s0 + q % B.spp_batch;
+  int p = B.slot0 + q;
+  if (q == 0) *B.count = B.act0 + B.n_paths;
+  int pix = B.pixels[B.p0 + lp];
+  Rng rng;
+  V3 o, dir;
+  float time;
+  camera_ray(S, pix, B.s_base + s, B.sobol[2 * s], B.sobol[2 * s + 1], B.nx, B.ny, B.base_seed, o, dir, time, rng);
   nts(&P.ray_o[p], make_float4(o.x, o.y, o.z, time));
   nts(&P.ray_d[p], make_float4(dir.x, dir.y, dir.z, 0.f));
   nts(&P.lcg[p], rng.lcg);
@@ -1456,38 +1464,23 @@ __device__ void finish_path(const PathState& P, int p, V3 C, int depth, uint64_t
   nts(&P.sample[3 * (size_t)p + 2], C.z);
 }
 
-// One hit of family F (color(), Raytracing_n.cpp:55-106).  Returns true when the
-// path continues with a new ray.
+// emitted() of the hit's material toward the incoming ray (material.h:348-354):
+// only diffuse_light emits, one-sided
+SRR_D V3 hit_emitted(const SceneView& S, int mat, V3 rdir, V3 hpt, V3 nrm, float hu, float hv) {
+  if (mat < 0) return v3(0.f);  // a null material* is UB in the reference: 0 here
+  const DMat& M = S.mats[mat];
+  if (M.kind == MAT_DIFFUSE_LIGHT && dot(nrm, rdir) < 0.0) return tex_value(S, M.tex, hu, hv, hpt);
+  return v3(0.f);
+}
+
+// The scattering half of one color() bounce for family F (Raytracing_n.cpp:63-94,
+// material.h): the next direction and time, and the bounce's record for the
+// back-to-front fold: (attenuation * scattering_pdf, pdf) or, specular,
+// (attenuation, 0) with `spec` set.
 template <int F>
-SRR_D bool shade_one(const SceneView& S, const PathState& P, int p, int max_depth) {
-  float4 ro = ntl(&P.ray_o[p]), rdv = ntl(&P.ray_d[p]);
-  V3 rdir = v3(rdv.x, rdv.y, rdv.z);
-  int depth = ntl(&P.depth[p]);
-  uint64_t spec = ntl(&P.spec[p]);
-  if (P.rays) P.rays[p] += 1;
-  const int mat = ntl(&P.hit_w[p]).w;
-  if (F == FAM_TERM) {
-    // miss -> vec3(0.0) (:104); a null material* is UB in the reference: 0 here;
-    // no scatter (light) or depth limit -> emitted (:97-100, material.h:348-354)
-    V3 emitted = v3(0.f);
-    if (mat >= 0) {
-      const DMat& M = S.mats[mat];
-      float4 hp = ntl(&P.hit_p[p]), hn = ntl(&P.hit_n[p]);
-      V3 nrm = v3(hn.x, hn.y, hn.z);
-      if (M.kind == MAT_DIFFUSE_LIGHT && dot(nrm, rdir) < 0.0)
-        emitted = tex_value(S, M.tex, hp.w, hn.w, v3(hp.x, hp.y, hp.z));
-    }
-    finish_path(P, p, emitted, depth, spec, max_depth);
-    return false;
-  }
-  float4 hp = ntl(&P.hit_p[p]), hn = ntl(&P.hit_n[p]);
-  V3 hpt = v3(hp.x, hp.y, hp.z), nrm = v3(hn.x, hn.y, hn.z);
-  float hu = hp.w, hv = hn.w;
-  const DMat M = S.mats[mat];
-  Rng rng{ntl(&P.lcg[p]), ntl(&P.pcg[p])};
-  V3 ndir;
-  float ntime = 0.0f;  // ray(a, b) defaults time to 0 (ray.h:10) for specular rays
-  size_t slot = (size_t)p * max_depth + depth;
+SRR_D void scatter(const SceneView& S, const DMat& M, V3 rdir, float rtime, V3 hpt, V3 nrm, float hu, float hv,
+                   Rng& rng, float4& rec, bool& spec, V3& ndir, float& ntime) {
+  ntime = 0.0f;  // ray(a, b) defaults time to 0 (ray.h:10) for specular rays
   if (F == FAM_SPEC) {
     V3 atten;
     if (M.kind == MAT_METAL) {  // material.h:248-256
@@ -1529,8 +1522,8 @@ SRR_D bool shade_one(const SceneView& S, const PathState& P, int p, int max_dept
       ndir = random_in_unit_sphere(rng);
       atten = tex_value(S, M.tex, hu, hv, hpt);
     }
-    nts(&P.rec_a[slot], make_float4(atten.x, atten.y, atten.z, 0.f));
-    spec |= (1ull << depth);
+    rec = make_float4(atten.x, atten.y, atten.z, 0.f);
+    spec = true;
   } else {
     // lambertian / orennayar / beckmann: mixture(light, bsdf) (Raytracing_n.cpp:73-94)
     V3 atten = tex_value(S, M.tex, hu, hv, hpt);
@@ -1557,9 +1550,43 @@ SRR_D bool shade_one(const SceneView& S, const PathState& P, int p, int max_dept
     }
     float spdf = scattering_pdf<F == FAM_BECK>(f, nrm, rdir, ndir);
     V3 as = atten * spdf;
-    nts(&P.rec_a[slot], make_float4(as.x, as.y, as.z, pdf_val));
-    ntime = ro.w;
+    rec = make_float4(as.x, as.y, as.z, pdf_val);
+    spec = false;
+    ntime = rtime;
   }
+}
+
+// One hit of family F (color(), Raytracing_n.cpp:55-106).  Returns true when the
+// path continues with a new ray.
+template <int F>
+SRR_D bool shade_one(const SceneView& S, const PathState& P, int p, int max_depth) {
+  float4 ro = ntl(&P.ray_o[p]), rdv = ntl(&P.ray_d[p]);
+  V3 rdir = v3(rdv.x, rdv.y, rdv.z);
+  int depth = ntl(&P.depth[p]);
+  uint64_t spec = ntl(&P.spec[p]);
+  if (P.rays) P.rays[p] += 1;
+  const int mat = ntl(&P.hit_w[p]).w;
+  if (F == FAM_TERM) {
+    // miss -> vec3(0.0) (:104); no scatter (light) or depth limit -> emitted (:97-100)
+    V3 emitted = v3(0.f);
+    if (mat >= 0) {
+      float4 hp = ntl(&P.hit_p[p]), hn = ntl(&P.hit_n[p]);
+      emitted = hit_emitted(S, mat, rdir, v3(hp.x, hp.y, hp.z), v3(hn.x, hn.y, hn.z), hp.w, hn.w);
+    }
+    finish_path(P, p, emitted, depth, spec, max_depth);
+    return false;
+  }
+  float4 hp = ntl(&P.hit_p[p]), hn = ntl(&P.hit_n[p]);
+  V3 hpt = v3(hp.x, hp.y, hp.z), nrm = v3(hn.x, hn.y, hn.z);
+  const DMat M = S.mats[mat];
+  Rng rng{ntl(&P.lcg[p]), ntl(&P.pcg[p])};
+  V3 ndir;
+  float ntime;
+  float4 rec;
+  bool sp;
+  scatter<F>(S, M, rdir, ro.w, hpt, nrm, hp.w, hn.w, rng, rec, sp, ndir, ntime);
+  nts(&P.rec_a[(size_t)p * max_depth + depth], rec);
+  if (sp) spec |= (1ull << depth);
   nts(&P.ray_o[p], make_float4(hpt.x, hpt.y, hpt.z, ntime));
   nts(&P.ray_d[p], make_float4(ndir.x, ndir.y, ndir.z, 0.f));
   nts(&P.lcg[p], rng.lcg);
@@ -1567,6 +1594,155 @@ SRR_D bool shade_one(const SceneView& S, const PathState& P, int p, int max_dept
   nts(&P.depth[p], depth + 1);
   nts(&P.spec[p], spec);
   return true;
+}
+
+// ===================================================== path-resident engine
+// One persistent kernel runs whole paths: each lane holds its path's ray, RNG
+// streams, depth and specular mask in registers across bounces (trace over the
+// LDS-staged world and the 4-wide BVH, hit record, material scatter), and when
+// its path ends it folds the bounce records back to front exactly like the
+// recursion returns, writes the sample and fetches the next (pixel, sample) from
+// a global cursor (one wave-aggregated atomic per refill).  No path state goes
+// through memory between bounces except the write-only bounce records.
+constexpr int kPathsBlock = 256;
+
+template <bool MEDIA, bool ALLFAM>
+__global__ void __launch_bounds__(kPathsBlock) k_paths(SceneView S0, PathWork W) {
+  SceneView S = S0;
+  constexpr int TR = TR_BVH4_PRUNE | TR_WL;
+  {
+    __shared__ uint4 s_world[kWorldLdsBytes / 16];
+    for (int i = threadIdx.x; i < S0.world_words; i += blockDim.x) s_world[i] = S0.world_blob[i];
+    __syncthreads();
+    const char* b = (const char*)s_world;
+    S.objs = (const DObj*)(b + S0.world_off[0]);
+    S.xforms = (const DXform*)(b + S0.world_off[1]);
+    S.spheres = (const DSphere*)(b + S0.world_off[2]);
+    S.rects = (const DRect*)(b + S0.world_off[3]);
+    S.stris = (const DStandaloneTri*)(b + S0.world_off[4]);
+    S.meshes = (const DMesh*)(b + S0.world_off[5]);
+    S.media = (const DMedium*)(b + S0.world_off[6]);
+  }
+  __shared__ int s_node[kStack * kPathsBlock];
+  __shared__ float s_t[kStack * kPathsBlock];
+  TraceCtx cx{nullptr, s_node + threadIdx.x, s_t + threadIdx.x};
+  const int slot = blockIdx.x * blockDim.x + threadIdx.x;
+  long long g = -1;  // path of this lane, -1 idle
+  bool exhausted = false;
+  Ray r{};
+  Rng rng{};
+  int depth = 0;
+  uint64_t spec = 0;
+  uint32_t prays = 0, nrays = 0;
+  for (;;) {
+    // refill lanes whose path ended
+    const bool need = g < 0 && !exhausted;
+    const uint64_t nm = __ballot(need);
+    if (nm) {
+      const int leader = __ffsll((unsigned long long)nm) - 1;
+      unsigned long long base = 0;
+      if (lane_id() == leader) base = atomicAdd(W.cursor, (unsigned long long)__popcll(nm));
+      base = __shfl(base, leader);
+      if (need) {
+        const long long idx = (long long)base + __popcll(nm & ((1ull << lane_id()) - 1));
+        if (idx < W.n_paths) {
+          g = idx;
+          const int lp = (int)(idx / W.spp_w), s = (int)(idx % W.spp_w);
+          if (lp >= W.npix || s >= W.spp_w) atomicOr(W.err, 1);
+          const int pix = W.pixels ? W.pixels[lp] : lp;
+          V3 o, d;
+          float tm;
+          camera_ray(S, pix, W.s_base + s, W.sobol[2 * s], W.sobol[2 * s + 1], W.nx, W.ny, W.base_seed, o, d, tm,
+                     rng);
+          r = Ray{o, d, tm};
+          depth = 0;
+          spec = 0;
+          prays = 0;
+        } else {
+          exhausted = true;
+        }
+      }
+    }
+    if (__ballot(g >= 0) == 0) break;
+    if (g >= 0) {
+      ++prays;
+      const WorldHit w = world_hit<MEDIA, TR>(S, r, rng, cx);
+      bool done = true;
+      V3 C = v3(0.f);
+      if (w.obj >= 0) {
+        const HitRec h = world_record<TR>(S, r, w);
+        const int kind = h.mat >= 0 ? S.mats[h.mat].kind : -1;
+        const int fam = family_of(h.mat, kind, depth, W.max_depth);
+        if (fam == FAM_TERM) {
+          C = hit_emitted(S, h.mat, r.d, h.p, h.n, h.u, h.v);
+        } else {
+          const DMat M = S.mats[h.mat];
+          float4 rec;
+          bool sp;
+          V3 nd;
+          float nt;
+          if (!ALLFAM || fam == FAM_DIFF) scatter<FAM_DIFF>(S, M, r.d, r.tm, h.p, h.n, h.u, h.v, rng, rec, sp, nd, nt);
+          else if (fam == FAM_BECK) scatter<FAM_BECK>(S, M, r.d, r.tm, h.p, h.n, h.u, h.v, rng, rec, sp, nd, nt);
+          else scatter<FAM_SPEC>(S, M, r.d, r.tm, h.p, h.n, h.u, h.v, rng, rec, sp, nd, nt);
+          if (depth >= W.max_depth || slot >= W.lanes) atomicOr(W.err, 2);
+          else nts(&W.rec[(size_t)depth * W.lanes + slot], rec);
+          if (sp) spec |= (1ull << depth);
+          r = Ray{h.p, nd, nt};
+          ++depth;
+          done = false;
+        }
+      }
+      if (done && (g >= W.n_paths || depth > W.max_depth)) {
+        atomicOr(W.err, 4);
+        g = -1;
+        done = false;
+      }
+      if (done) {
+        // fold the bounces back to front (Raytracing_n.cpp:69, :94), as finish_path
+        for (int k = depth - 1; k >= 0; --k) {
+          const float4 a = ntl(&W.rec[(size_t)k * W.lanes + slot]);
+          const V3 av = v3(a.x, a.y, a.z);
+          if ((spec >> k) & 1) C = av * C;
+          else C = v3(0.f) + (av * C) / a.w;
+        }
+        if (W.raw) {
+          W.raw[3 * g] = C.x;
+          W.raw[3 * g + 1] = C.y;
+          W.raw[3 * g + 2] = C.z;
+        }
+        if (W.rays) W.rays[g] = (uint8_t)prays;
+        if (!(C.x == C.x)) C.x = 0;  // de_nan (Raytracing_n.cpp:47-53)
+        if (!(C.y == C.y)) C.y = 0;
+        if (!(C.z == C.z)) C.z = 0;
+        nts(&W.sample[3 * g], C.x);
+        nts(&W.sample[3 * g + 1], C.y);
+        nts(&W.sample[3 * g + 2], C.z);
+        nrays += prays;
+        g = -1;
+      }
+    }
+  }
+  unsigned long long tot = nrays;
+  for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
+  if (lane_id() == 0 && tot) atomicAdd(W.counters, tot);
+}
+
+// acc[pixel] += the window's samples in sample order (the sum order of
+// k_accumulate, Raytracing_n.cpp:841)
+__global__ void __launch_bounds__(256) k_accumulate_window(const float* sample, int npix, int spp_w, float* acc) {
+  const int lp = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lp >= npix) return;
+  const size_t a = 3 * (size_t)lp;
+  float cx = acc[a], cy = acc[a + 1], cz = acc[a + 2];
+  const float* sp = sample + 3 * (size_t)lp * spp_w;
+  for (int s = 0; s < spp_w; ++s) {
+    cx += ntl(&sp[3 * s]);
+    cy += ntl(&sp[3 * s + 1]);
+    cz += ntl(&sp[3 * s + 2]);
+  }
+  acc[a] = cx;
+  acc[a + 1] = cy;
+  acc[a + 2] = cz;
 }
 
 constexpr int kMaxRegions = 8;
@@ -1771,6 +1947,35 @@ void launch_accumulate(const PathState& P, const BatchInfo& B, float* acc, hipSt
 void launch_finish(const float* acc, float* mean, int64_t n, int ns, hipStream_t st) {
   int64_t g = (3 * n + 255) / 256;
   hipLaunchKernelGGL(dev::k_finish, dim3((unsigned)g), dim3(256), 0, st, acc, mean, n, ns);
+}
+
+
+int paths_lanes_per_device(const SceneView& S, int device) {
+  (void)S;
+  int cus = 0, per_cu = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)dev::k_paths<false, true>,
+                                                   dev::kPathsBlock, 0) != hipSuccess || per_cu <= 0)
+    per_cu = 2;
+  return cus * per_cu * dev::kPathsBlock;
+}
+
+void launch_paths(const SceneView& S, const PathWork& W, int all_families, hipStream_t st) {
+  const int blocks = W.lanes / dev::kPathsBlock;
+#define SRR_LAUNCH_PATHS(M, A) \
+  hipLaunchKernelGGL((dev::k_paths<M, A>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W)
+  if (S.has_media) {
+    if (all_families) SRR_LAUNCH_PATHS(true, true);
+    else SRR_LAUNCH_PATHS(true, false);
+  } else {
+    if (all_families) SRR_LAUNCH_PATHS(false, true);
+    else SRR_LAUNCH_PATHS(false, false);
+  }
+#undef SRR_LAUNCH_PATHS
+}
+
+void launch_accumulate_window(const float* sample, int npix, int spp_w, float* acc, hipStream_t st) {
+  hipLaunchKernelGGL(dev::k_accumulate_window, dim3((npix + 255) / 256), dim3(256), 0, st, sample, npix, spp_w, acc);
 }
 
 }  // namespace srr

@@ -105,6 +105,9 @@ int renderer_create(const Scene& sc, int device, srr_renderer** out, std::string
   V.lights = li;
   V.n_lights = (int)F.lights.size();
   V.cam = cm;
+  r->diffuse_only = true;
+  for (const DMat& m : F.mats)
+    if (m.kind != MAT_LAMBERTIAN && m.kind != MAT_ORENNAYAR && m.kind != MAT_DIFFUSE_LIGHT) r->diffuse_only = false;
   RCHK(hipStreamCreateWithFlags(&r->acc_st, hipStreamNonBlocking));
   RCHK(hipEventCreate(&r->ev_beg));
   RCHK(hipEventCreate(&r->ev_end));
@@ -171,8 +174,151 @@ static int ensure_lane(Lane& L, size_t n, int depth, bool keep, std::string& err
   return 0;
 }
 
+// Path-resident engine (kernels.hip k_paths): one persistent kernel per window
+// of samples; samples land in a [pixel][sample] buffer that k_accumulate_window
+// sums in sample order, so the image is bitwise the wavefront engine's.
+static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix, int64_t npix, float* d_mean,
+                        srr_stats* stats, std::string& err) {
+  const bool keep = (p->flags & SRR_FLAG_KEEP_PATHS) != 0;
+  hipStream_t st = r->acc_st;
+  const auto t_host0 = std::chrono::steady_clock::now();
+  srr_stats s{};
+  // pixels: identity for a whole frame, else the shard list
+  bool identity = p->shard_count <= 1;
+  for (int64_t i = 0; identity && i < npix; i += std::max<int64_t>(1, npix / 64)) identity = pix[i] == i;
+  if ((size_t)npix > r->pix_cap) {
+    (void)hipFree(r->pixels);
+    (void)hipFree(r->acc);
+    r->pixels = nullptr;
+    r->acc = nullptr;
+    RCHK(hipMalloc((void**)&r->pixels, npix * sizeof(int32_t)));
+    RCHK(hipMalloc((void**)&r->acc, 3 * npix * sizeof(float)));
+    r->pix_cap = npix;
+  }
+  if (!identity) RCHK(hipMemcpy(r->pixels, pix, npix * sizeof(int32_t), hipMemcpyHostToDevice));
+  const int n_sobol = p->sample_begin + p->spp;
+  if (n_sobol > r->sobol_n) {
+    (void)hipFree(r->sobol);
+    r->sobol = nullptr;
+    RCHK(hipMalloc((void**)&r->sobol, 2 * (size_t)n_sobol * sizeof(double)));
+    r->sobol_n = n_sobol;
+  }
+  std::vector<double> sp(2 * (size_t)n_sobol);
+  sobol2((unsigned)n_sobol, sp.data());
+  RCHK(hipMemcpy(r->sobol, sp.data(), sp.size() * sizeof(double), hipMemcpyHostToDevice));
+  if (keep) {
+    size_t need = (size_t)npix * p->spp;
+    if (need > r->keep_cap) {
+      (void)hipFree(r->raw_all);
+      (void)hipFree(r->rays_all);
+      RCHK(hipMalloc((void**)&r->raw_all, need * 3 * sizeof(float)));
+      RCHK(hipMalloc((void**)&r->rays_all, need));
+      r->keep_cap = need;
+    }
+    r->kept_paths = (int64_t)need;
+  }
+  // persistent lanes and their bounce records
+  if (!r->pw_lanes) r->pw_lanes = paths_lanes_per_device(r->view, r->device);
+  const size_t rec_need = (size_t)r->pw_lanes * std::max(1, p->max_depth);
+  if (rec_need > r->pw_rec_cap) {
+    (void)hipFree(r->pw_rec);
+    r->pw_rec = nullptr;
+    RCHK(hipMalloc((void**)&r->pw_rec, rec_need * sizeof(float4)));
+    r->pw_rec_cap = rec_need;
+  }
+  // sample window: all pixels x W samples, buffer within SRR_WINDOW_MB (default 2048)
+  size_t budget = (size_t)2048 << 20;
+  if (const char* e = getenv("SRR_WINDOW_MB")) budget = (size_t)std::max(1, atoi(e)) << 20;
+  const int W = (int)std::max<int64_t>(1, std::min<int64_t>(p->spp, (int64_t)(budget / (12 * (size_t)npix))));
+  const size_t win_paths = (size_t)npix * W;
+  if (win_paths > r->pw_sample_cap) {
+    (void)hipFree(r->pw_sample);
+    (void)hipFree(r->pw_raw);
+    (void)hipFree(r->pw_rays);
+    r->pw_sample = r->pw_raw = nullptr;
+    r->pw_rays = nullptr;
+    RCHK(hipMalloc((void**)&r->pw_sample, win_paths * 3 * sizeof(float)));
+    r->pw_sample_cap = win_paths;
+  }
+  if (keep && !r->pw_raw) {
+    RCHK(hipMalloc((void**)&r->pw_raw, r->pw_sample_cap * 3 * sizeof(float)));
+    RCHK(hipMalloc((void**)&r->pw_rays, r->pw_sample_cap));
+  }
+  if (!r->pw_ctr) RCHK(hipMalloc((void**)&r->pw_ctr, 3 * sizeof(unsigned long long)));
+  RCHK(hipMemsetAsync(r->pw_ctr, 0, 3 * sizeof(unsigned long long), st));
+  RCHK(hipMemsetAsync(r->acc, 0, 3 * npix * sizeof(float), st));
+  const bool all_fam = !r->diffuse_only;
+  RCHK(hipEventRecord(r->ev_beg, st));
+  double kernel_ms = 0;
+  for (int s0 = 0; s0 < p->spp; s0 += W) {
+    const int Wn = std::min(W, p->spp - s0);
+    PathWork w{};
+    w.pixels = identity ? nullptr : r->pixels;
+    w.sobol = r->sobol + 2 * (size_t)(p->sample_begin + s0);
+    w.npix = (int)npix;
+    w.spp_w = Wn;
+    w.s_base = p->sample_begin + s0;
+    w.nx = p->nx;
+    w.ny = p->ny;
+    w.base_seed = p->base_seed;
+    w.n_paths = (int64_t)npix * Wn;
+    w.max_depth = p->max_depth;
+    w.cursor = r->pw_ctr + 1;
+    w.counters = r->pw_ctr;
+    w.sample = r->pw_sample;
+    w.raw = keep ? r->pw_raw : nullptr;
+    w.rays = keep ? r->pw_rays : nullptr;
+    w.rec = r->pw_rec;
+    w.err = (int*)(r->pw_ctr + 2);
+    w.lanes = (int)std::min<int64_t>(r->pw_lanes, ((w.n_paths + 255) / 256) * 256);
+    RCHK(hipMemsetAsync(w.cursor, 0, sizeof(unsigned long long), st));
+    RCHK(hipEventRecord(r->lanes[0].ev_t0, st));
+    launch_paths(r->view, w, all_fam ? 1 : 0, st);
+    RCHK(hipEventRecord(r->lanes[0].ev_t1, st));
+    launch_accumulate_window(r->pw_sample, (int)npix, Wn, r->acc, st);
+    if (keep) {
+      RCHK(hipMemcpy2DAsync(r->raw_all + 3 * (size_t)s0, 3 * sizeof(float) * p->spp, r->pw_raw,
+                            3 * sizeof(float) * Wn, 3 * sizeof(float) * Wn, npix, hipMemcpyDeviceToDevice, st));
+      RCHK(hipMemcpy2DAsync(r->rays_all + s0, p->spp, r->pw_rays, Wn, Wn, npix, hipMemcpyDeviceToDevice, st));
+    }
+    RCHK(hipEventSynchronize(r->lanes[0].ev_t1));
+    float ms = 0;
+    RCHK(hipEventElapsedTime(&ms, r->lanes[0].ev_t0, r->lanes[0].ev_t1));
+    kernel_ms += ms;
+    s.trace_launches += 1;
+  }
+  launch_finish(r->acc, d_mean, npix, p->spp, st);
+  RCHK(hipEventRecord(r->ev_end, st));
+  RCHK(hipStreamSynchronize(st));
+  RCHK(hipGetLastError());
+  unsigned long long ctr[3] = {0, 0, 0};
+  RCHK(hipMemcpy(ctr, r->pw_ctr, sizeof(ctr), hipMemcpyDeviceToHost));
+  const unsigned long long rays = ctr[0];
+  if (ctr[2]) {
+    err = "k_paths index guard tripped (bits " + std::to_string(ctr[2]) + ")";
+    return SRR_EIO;
+  }
+  float total = 0;
+  RCHK(hipEventElapsedTime(&total, r->ev_beg, r->ev_end));
+  s.world_rays = (int64_t)rays;
+  s.paths = npix * p->spp;
+  s.trace_ms = kernel_ms;
+  s.total_ms = total;
+  (void)t_host0;
+  if (stats) *stats = s;
+  return 0;
+}
+
 int render_device(srr_renderer* r, const srr_params* p, const int32_t* pix, int64_t npix, float* d_mean,
                   srr_stats* stats, std::string& err) {
+  static const bool wave_engine = [] {
+    const char* e = getenv("SRR_ENGINE");
+    return e && !strcmp(e, "wave");
+  }();
+  // the path engine stages the world tables in LDS (kernels.hip kWorldLdsBytes)
+  const bool fits = (size_t)r->view.world_words * 16 <= (size_t)kPathsWorldLdsBytes;
+  if (!wave_engine && fits && !(p->flags & SRR_FLAG_COUNT_VISITS))
+    return render_paths(r, p, pix, npix, d_mean, stats, err);
   RCHK(hipSetDevice(r->device));
   const bool keep = (p->flags & SRR_FLAG_KEEP_PATHS) != 0;
   const int R = kRegionsPerLane;
@@ -415,6 +561,11 @@ srr_renderer::~srr_renderer() {
   (void)hipDeviceSynchronize();
   for (void* p : scene_bufs) (void)hipFree(p);
   if (visits) (void)hipFree(visits);
+  (void)hipFree(pw_rec);
+  (void)hipFree(pw_sample);
+  (void)hipFree(pw_raw);
+  (void)hipFree(pw_rays);
+  (void)hipFree(pw_ctr);
   for (auto& L : lanes) {
     srr::free_lane_paths(L);
     (void)hipFree(L.cnt);

@@ -59,6 +59,16 @@ struct srr_renderer {
   // frame buffers
   float* acc = nullptr;
   unsigned long long* visits = nullptr;  // SRR_FLAG_COUNT_VISITS counters (3)
+  // path-resident engine (render_paths)
+  int pw_lanes = 0;
+  bool diffuse_only = false;  // no beckmann / specular materials: lean kernel variant
+  float4* pw_rec = nullptr;
+  size_t pw_rec_cap = 0;
+  float* pw_sample = nullptr;
+  float* pw_raw = nullptr;
+  uint8_t* pw_rays = nullptr;
+  size_t pw_sample_cap = 0;
+  unsigned long long* pw_ctr = nullptr;  // [0] world rays, [1] path cursor
   int32_t* pixels = nullptr;
   size_t pix_cap = 0;
   double* sobol = nullptr;
