@@ -72,8 +72,9 @@ struct BatchInfo {
 };
 
 // One window of a frame for the path-resident persistent kernel (k_paths):
-// every (pixel, sample) of pixels x [0, spp_w) is a path, numbered
-// g = lp * spp_w + s; lanes fetch g from `cursor` as their paths finish.
+// every (pixel, sample) of pixels x [0, spp_w) is a path, numbered pixel-major
+// g = lp * spp_w + s (a wave's lanes take samples of one pixel: coherent first
+// bounces); lanes fetch g from `cursor` as their paths finish.
 struct PathWork {
   const int32_t* pixels;  // shard pixel list (PPM-order indices), nullptr = identity
   const double* sobol;    // [spp_w][2], window sample 0 first
@@ -85,9 +86,10 @@ struct PathWork {
   int max_depth;
   unsigned long long* cursor;  // next path to start (device, zeroed per window)
   unsigned long long* counters;  // [0] += world rays traced
-  float* sample;          // [n_paths][3] de_nan'd radiance
-  float* raw;             // optional [n_paths][3] radiance before de_nan
-  uint8_t* rays;          // optional [n_paths] world rays per path
+  float* sample;          // [n_paths][3] de_nan'd radiance, index g
+  float* raw;             // optional kept paths [npix][keep_spp][3] before de_nan
+  uint8_t* rays;          // optional kept [npix][keep_spp] world rays per path
+  int keep_spp, keep_s0;  // frame spp and this window's first sample in them
   float4* rec;            // bounce records [max_depth][lanes]
   int lanes;              // persistent lanes (grid * block)
   int* err;               // guard bits set on an out-of-range index (never expected)

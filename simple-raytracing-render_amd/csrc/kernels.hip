@@ -1606,8 +1606,8 @@ SRR_D bool shade_one(const SceneView& S, const PathState& P, int p, int max_dept
 // through memory between bounces except the write-only bounce records.
 constexpr int kPathsBlock = 256;
 
-template <bool MEDIA, bool ALLFAM>
-__global__ void __launch_bounds__(kPathsBlock) k_paths(SceneView S0, PathWork W) {
+template <bool MEDIA, bool ALLFAM, int MINB>
+__global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathWork W) {
   SceneView S = S0;
   constexpr int TR = TR_BVH4_PRUNE | TR_WL;
   {
@@ -1647,7 +1647,7 @@ __global__ void __launch_bounds__(kPathsBlock) k_paths(SceneView S0, PathWork W)
         const long long idx = (long long)base + __popcll(nm & ((1ull << lane_id()) - 1));
         if (idx < W.n_paths) {
           g = idx;
-          const int lp = (int)(idx / W.spp_w), s = (int)(idx % W.spp_w);
+          const int lp = (int)(idx / W.spp_w), s = (int)(idx % W.spp_w);  // pixel-major: g = lp * spp_w + s
           if (lp >= W.npix || s >= W.spp_w) atomicOr(W.err, 1);
           const int pix = W.pixels ? W.pixels[lp] : lp;
           V3 o, d;
@@ -1705,12 +1705,13 @@ __global__ void __launch_bounds__(kPathsBlock) k_paths(SceneView S0, PathWork W)
           if ((spec >> k) & 1) C = av * C;
           else C = v3(0.f) + (av * C) / a.w;
         }
-        if (W.raw) {
-          W.raw[3 * g] = C.x;
-          W.raw[3 * g + 1] = C.y;
-          W.raw[3 * g + 2] = C.z;
+        if (W.raw) {  // kept paths: [pixel][sample of the frame]
+          const size_t kq = (size_t)(g / W.spp_w) * W.keep_spp + W.keep_s0 + (size_t)(g % W.spp_w);
+          W.raw[3 * kq] = C.x;
+          W.raw[3 * kq + 1] = C.y;
+          W.raw[3 * kq + 2] = C.z;
+          W.rays[kq] = (uint8_t)prays;
         }
-        if (W.rays) W.rays[g] = (uint8_t)prays;
         if (!(C.x == C.x)) C.x = 0;  // de_nan (Raytracing_n.cpp:47-53)
         if (!(C.y == C.y)) C.y = 0;
         if (!(C.z == C.z)) C.z = 0;
@@ -1728,7 +1729,7 @@ __global__ void __launch_bounds__(kPathsBlock) k_paths(SceneView S0, PathWork W)
 }
 
 // acc[pixel] += the window's samples in sample order (the sum order of
-// k_accumulate, Raytracing_n.cpp:841)
+// k_accumulate, Raytracing_n.cpp:841); samples are [pixel][sample]
 __global__ void __launch_bounds__(256) k_accumulate_window(const float* sample, int npix, int spp_w, float* acc) {
   const int lp = blockIdx.x * blockDim.x + threadIdx.x;
   if (lp >= npix) return;
@@ -1950,27 +1951,51 @@ void launch_finish(const float* acc, float* mean, int64_t n, int ns, hipStream_t
 }
 
 
+// Occupancy of the path kernel: min resident 256-thread blocks per CU (2-6,
+// SRR_PATHS_OCC).  The kernel's natural allocation is ~226 VGPRs (2 waves per
+// SIMD); capping registers spills some cold state to scratch but hides more
+// latency -- measured on C2: 2 -> 5.25, 3 -> 6.10, 4 -> 6.49 Gsamples/s.
+constexpr int kPathsOccDefault = 4;
+static int paths_min_blocks() {
+  static const int v = [] {
+    const char* e = getenv("SRR_PATHS_OCC");
+    int x = e ? atoi(e) : kPathsOccDefault;
+    return x >= 2 && x <= 6 ? x : kPathsOccDefault;
+  }();
+  return v;
+}
+
 int paths_lanes_per_device(const SceneView& S, int device) {
   (void)S;
   int cus = 0, per_cu = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)dev::k_paths<false, true>,
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)dev::k_paths<false, false, 2>,
                                                    dev::kPathsBlock, 0) != hipSuccess || per_cu <= 0)
     per_cu = 2;
+  per_cu = std::max(per_cu, paths_min_blocks());
   return cus * per_cu * dev::kPathsBlock;
 }
 
 void launch_paths(const SceneView& S, const PathWork& W, int all_families, hipStream_t st) {
   const int blocks = W.lanes / dev::kPathsBlock;
-#define SRR_LAUNCH_PATHS(M, A) \
-  hipLaunchKernelGGL((dev::k_paths<M, A>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W)
-  if (S.has_media) {
-    if (all_families) SRR_LAUNCH_PATHS(true, true);
-    else SRR_LAUNCH_PATHS(true, false);
-  } else {
-    if (all_families) SRR_LAUNCH_PATHS(false, true);
-    else SRR_LAUNCH_PATHS(false, false);
+#define SRR_LAUNCH_PATHS(M, A, B) \
+  hipLaunchKernelGGL((dev::k_paths<M, A, B>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W)
+#define SRR_LAUNCH_PATHS_B(M, A)                          \
+  switch (paths_min_blocks()) {                           \
+    case 2: SRR_LAUNCH_PATHS(M, A, 2); break;             \
+    case 3: SRR_LAUNCH_PATHS(M, A, 3); break;             \
+    case 5: SRR_LAUNCH_PATHS(M, A, 5); break;             \
+    case 6: SRR_LAUNCH_PATHS(M, A, 6); break;             \
+    default: SRR_LAUNCH_PATHS(M, A, 4); break;            \
   }
+  if (S.has_media) {
+    if (all_families) { SRR_LAUNCH_PATHS_B(true, true) }
+    else { SRR_LAUNCH_PATHS_B(true, false) }
+  } else {
+    if (all_families) { SRR_LAUNCH_PATHS_B(false, true) }
+    else { SRR_LAUNCH_PATHS_B(false, false) }
+  }
+#undef SRR_LAUNCH_PATHS_B
 #undef SRR_LAUNCH_PATHS
 }
 

@@ -176,7 +176,7 @@ static int ensure_lane(Lane& L, size_t n, int depth, bool keep, std::string& err
 
 // Path-resident engine (kernels.hip k_paths): one persistent kernel per window
 // of samples; samples land in a [pixel][sample] buffer that k_accumulate_window
-// sums in sample order, so the image is bitwise the wavefront engine's.
+// sums per pixel in sample order, so the image is bitwise the wavefront engine's.
 static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix, int64_t npix, float* d_mean,
                         srr_stats* stats, std::string& err) {
   const bool keep = (p->flags & SRR_FLAG_KEEP_PATHS) != 0;
@@ -226,8 +226,8 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
     RCHK(hipMalloc((void**)&r->pw_rec, rec_need * sizeof(float4)));
     r->pw_rec_cap = rec_need;
   }
-  // sample window: all pixels x W samples, buffer within SRR_WINDOW_MB (default 2048)
-  size_t budget = (size_t)2048 << 20;
+  // sample window: all pixels x W samples, buffer within SRR_WINDOW_MB (default 8192)
+  size_t budget = (size_t)8192 << 20;
   if (const char* e = getenv("SRR_WINDOW_MB")) budget = (size_t)std::max(1, atoi(e)) << 20;
   const int W = (int)std::max<int64_t>(1, std::min<int64_t>(p->spp, (int64_t)(budget / (12 * (size_t)npix))));
   const size_t win_paths = (size_t)npix * W;
@@ -239,10 +239,6 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
     r->pw_rays = nullptr;
     RCHK(hipMalloc((void**)&r->pw_sample, win_paths * 3 * sizeof(float)));
     r->pw_sample_cap = win_paths;
-  }
-  if (keep && !r->pw_raw) {
-    RCHK(hipMalloc((void**)&r->pw_raw, r->pw_sample_cap * 3 * sizeof(float)));
-    RCHK(hipMalloc((void**)&r->pw_rays, r->pw_sample_cap));
   }
   if (!r->pw_ctr) RCHK(hipMalloc((void**)&r->pw_ctr, 3 * sizeof(unsigned long long)));
   RCHK(hipMemsetAsync(r->pw_ctr, 0, 3 * sizeof(unsigned long long), st));
@@ -266,8 +262,10 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
     w.cursor = r->pw_ctr + 1;
     w.counters = r->pw_ctr;
     w.sample = r->pw_sample;
-    w.raw = keep ? r->pw_raw : nullptr;
-    w.rays = keep ? r->pw_rays : nullptr;
+    w.raw = keep ? r->raw_all : nullptr;
+    w.rays = keep ? r->rays_all : nullptr;
+    w.keep_spp = p->spp;
+    w.keep_s0 = s0;
     w.rec = r->pw_rec;
     w.err = (int*)(r->pw_ctr + 2);
     w.lanes = (int)std::min<int64_t>(r->pw_lanes, ((w.n_paths + 255) / 256) * 256);
@@ -276,11 +274,6 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
     launch_paths(r->view, w, all_fam ? 1 : 0, st);
     RCHK(hipEventRecord(r->lanes[0].ev_t1, st));
     launch_accumulate_window(r->pw_sample, (int)npix, Wn, r->acc, st);
-    if (keep) {
-      RCHK(hipMemcpy2DAsync(r->raw_all + 3 * (size_t)s0, 3 * sizeof(float) * p->spp, r->pw_raw,
-                            3 * sizeof(float) * Wn, 3 * sizeof(float) * Wn, npix, hipMemcpyDeviceToDevice, st));
-      RCHK(hipMemcpy2DAsync(r->rays_all + s0, p->spp, r->pw_rays, Wn, Wn, npix, hipMemcpyDeviceToDevice, st));
-    }
     RCHK(hipEventSynchronize(r->lanes[0].ev_t1));
     float ms = 0;
     RCHK(hipEventElapsedTime(&ms, r->lanes[0].ev_t0, r->lanes[0].ev_t1));
