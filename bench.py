@@ -146,10 +146,15 @@ def main():
         # roofline of the dominant kernel (srr_trace) on rank 0: algorithmic bytes
         # (B_cfg per world ray, reference traversal counts) over its HIP-event time
         achieved = rays * b_cfg / (trace_ms * 1e-3) / 1e9 if trace_ms > 0 else None
+        wave = bool(os.environ.get("SRR_ENGINE") == "wave")
+        kernel_name = ("k_trace (wavefront engine)" if wave else
+                       "k_paths (path-resident persistent kernel: trace + shade)")
         traffic = None
         pmc = os.path.join(ROOT, "profiles", f"pmc_{a.scene}.json")
         if os.path.exists(pmc):
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+            pj = json.load(open(pmc))
+            if pj.get("kernel", "") in kernel_name:
+                traffic = pj.get("hbm_bytes_per_launch")
         out = {
             "metric": "Msamples/s (rays x bounces) + HBM GB/s vs roofline, Cornell+teapot 1024spp",
             "value": round(value, 3),
@@ -173,7 +178,7 @@ def main():
                        "parallelism": f"{a.plan}{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                         "traffic": traffic, "kernel": "srr_trace (k_trace)", "B_cfg": round(b_cfg, 1),
+                         "traffic": traffic, "kernel": kernel_name, "B_cfg": round(b_cfg, 1),
                          "trace_ms_per_launch": round(trace_ms / max(launches, 1), 4)},
         }
         if a.count_visits:

@@ -130,6 +130,8 @@ typedef struct srr_params {
 #define SRR_FLAG_SORT_MATERIALS 1 /* material-sorted shading (perf only)      */
 #define SRR_FLAG_KEEP_PATHS 2     /* keep per-path radiance for parity tests   */
 #define SRR_FLAG_COUNT_VISITS 4   /* count mesh box / triangle tests (slower)    */
+#define SRR_FLAG_WAVEFRONT 8      /* use the wavefront engine (per-bounce kernels) */
+                                  /* instead of the path-resident persistent one  */
 
 typedef struct srr_stats {
   int64_t world_rays;   /* world->hit calls (the metric's samples)             */

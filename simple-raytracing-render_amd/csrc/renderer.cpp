@@ -304,10 +304,11 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
 
 int render_device(srr_renderer* r, const srr_params* p, const int32_t* pix, int64_t npix, float* d_mean,
                   srr_stats* stats, std::string& err) {
-  static const bool wave_engine = [] {
+  static const bool wave_env = [] {
     const char* e = getenv("SRR_ENGINE");
     return e && !strcmp(e, "wave");
   }();
+  const bool wave_engine = wave_env || (p->flags & SRR_FLAG_WAVEFRONT);
   // the path engine stages the world tables in LDS (kernels.hip kWorldLdsBytes)
   const bool fits = (size_t)r->view.world_words * 16 <= (size_t)kPathsWorldLdsBytes;
   if (!wave_engine && fits && !(p->flags & SRR_FLAG_COUNT_VISITS))

@@ -16,6 +16,7 @@ _LIB = None
 FLAG_SORT_MATERIALS = 1
 FLAG_KEEP_PATHS = 2
 FLAG_COUNT_VISITS = 4
+FLAG_WAVEFRONT = 8
 
 
 class SrrError(RuntimeError):

@@ -27,10 +27,15 @@ def golden(name):
     return m, text, paths, rays, img
 
 
+ENGINES = {"paths": 0, "wavefront": capi.FLAG_WAVEFRONT}
+
+
+@pytest.mark.parametrize("engine", sorted(ENGINES))
 @pytest.mark.parametrize("name", sorted(META))
-def test_paths_match_reference(name):
+def test_paths_match_reference(name, engine):
     m, text, gp, gr, gi = golden(name)
-    out = capi.Renderer(text).render(m["nx"], m["ny"], m["spp"], m["max_depth"], keep_paths=True)
+    out = capi.Renderer(text).render(m["nx"], m["ny"], m["spp"], m["max_depth"], keep_paths=True,
+                                     flags=ENGINES[engine])
     pc = parity.compare_paths(out["paths"], gp)
     ic = parity.compare_images(out["mean"], gi)
     rays_eq = float((out["rays"] == gr).mean())
@@ -40,6 +45,17 @@ def test_paths_match_reference(name):
     assert rays_eq >= parity.MIN_MATCH
     assert abs(out["stats"]["world_rays"] - m["world_rays"]) <= 0.01 * m["world_rays"]
     assert ic["mean_rel"] <= 0.005, ic
+
+
+@pytest.mark.parametrize("factory", [scenes.s2_cornell_teapot, lambda: scenes.s3_cornell_teapot_microfacet("metal")])
+def test_engines_render_identical_images(factory):
+    """The path-resident and wavefront engines run the same per-path arithmetic
+    and sum each pixel's samples in the same order: bitwise equal images."""
+    sc, _ = factory()
+    r = capi.Renderer(sc.text())
+    a = r.render(40, 32, 12, 50)["mean"]
+    b = r.render(40, 32, 12, 50, flags=capi.FLAG_WAVEFRONT)["mean"]
+    np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
 
 
 def test_shards_assemble_to_the_same_image():

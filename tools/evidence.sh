@@ -16,7 +16,7 @@ for c in FETCH_SIZE WRITE_SIZE; do
     python $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --scene $SCENE > $O/$TAG.pmc_$c.log 2>&1 \
     || { echo "pmc $c failed"; tail -5 $O/$TAG.pmc_$c.log; exit 1; }
 done
-python $R/tools/pmc_traffic.py $O/$TAG.pmc_FETCH_SIZE $O/$TAG.pmc_WRITE_SIZE k_trace $O/pmc_$SCENE.json || exit 1
+python $R/tools/pmc_traffic.py $O/$TAG.pmc_FETCH_SIZE $O/$TAG.pmc_WRITE_SIZE k_paths $O/pmc_$SCENE.json || exit 1
 cp $O/pmc_$SCENE.json $R/profiles/pmc_$SCENE.json
 cd $R
 timeout -k 10 600 python bench.py --scene $SCENE > $O/$TAG.bench.log 2>&1 || { tail -5 $O/$TAG.bench.log; exit 1; }
