@@ -1729,18 +1729,40 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
 }
 
 // acc[pixel] += the window's samples in sample order (the sum order of
-// k_accumulate, Raytracing_n.cpp:841); samples are [pixel][sample]
+// k_accumulate, Raytracing_n.cpp:841).  Samples are [pixel][sample]; a block
+// stages 256 pixels x 16 samples through LDS with coalesced loads, then each
+// thread adds its own pixel's samples in order.
+constexpr int kAccChunk = 16;
 __global__ void __launch_bounds__(256) k_accumulate_window(const float* sample, int npix, int spp_w, float* acc) {
-  const int lp = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ float tile[256 * (3 * kAccChunk + 1)];
+  const int p0 = blockIdx.x * 256;
+  const int lp = p0 + threadIdx.x;
+  const int np = min(256, npix - p0);
+  float cx = 0, cy = 0, cz = 0;
+  if (lp < npix) {
+    cx = acc[3 * (size_t)lp];
+    cy = acc[3 * (size_t)lp + 1];
+    cz = acc[3 * (size_t)lp + 2];
+  }
+  for (int s0 = 0; s0 < spp_w; s0 += kAccChunk) {
+    const int n = min(kAccChunk, spp_w - s0), row = 3 * n;
+    for (int i = threadIdx.x; i < np * row; i += 256) {
+      const int px = i / row, f = i - px * row;
+      tile[px * (3 * kAccChunk + 1) + f] = ntl(&sample[((size_t)(p0 + px) * spp_w + s0) * 3 + f]);
+    }
+    __syncthreads();
+    if (lp < npix) {
+      const float* t = &tile[threadIdx.x * (3 * kAccChunk + 1)];
+      for (int k = 0; k < n; ++k) {
+        cx += t[3 * k];
+        cy += t[3 * k + 1];
+        cz += t[3 * k + 2];
+      }
+    }
+    __syncthreads();
+  }
   if (lp >= npix) return;
   const size_t a = 3 * (size_t)lp;
-  float cx = acc[a], cy = acc[a + 1], cz = acc[a + 2];
-  const float* sp = sample + 3 * (size_t)lp * spp_w;
-  for (int s = 0; s < spp_w; ++s) {
-    cx += ntl(&sp[3 * s]);
-    cy += ntl(&sp[3 * s + 1]);
-    cz += ntl(&sp[3 * s + 2]);
-  }
   acc[a] = cx;
   acc[a + 1] = cy;
   acc[a + 2] = cz;
