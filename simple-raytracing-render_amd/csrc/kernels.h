@@ -31,12 +31,12 @@ struct SceneView {  // device pointers into the flattened tables (device_scene.h
   const DLight* lights;
   int n_lights;
   const DCamera* cam;
-  // the world traversal's tables packed in one blob (16-B aligned pieces) that
-  // the trace kernel copies to LDS when it is small: byte offsets of objs,
-  // xforms, spheres, rects, stris, meshes, media
+  // the world traversal's and shading's small tables packed in one blob (16-B
+  // aligned pieces) that the kernels copy to LDS: byte offsets of objs, xforms,
+  // spheres, rects, stris, meshes, media, mats, texs, lights
   const uint4* world_blob;
   int world_words;  // 16-B words
-  int world_off[7];
+  int world_off[10];
 };
 
 // Struct-of-arrays state of the paths of one batch (capacity N).

@@ -863,8 +863,10 @@ SRR_D V3 random_cosine_direction(Rng& rng) {
   float r2 = drand(rng);
   float phi = 2 * kPi * r1;
   float z = rsqrt_exact(1 - r2);
-  float x = rcos(phi) * 2 * rsqrt_exact(r2);
-  float y = rsin(phi) * 2 * rsqrt_exact(r2);
+  double sp, cp;  // cos / sin of the same float (evaluated in double, rounded once: rcos / rsin)
+  ::sincos((double)phi, &sp, &cp);
+  float x = (float)cp * 2 * rsqrt_exact(r2);
+  float y = (float)sp * 2 * rsqrt_exact(r2);
   return v3(x, y, z);
 }
 
@@ -1606,8 +1608,11 @@ SRR_D bool shade_one(const SceneView& S, const PathState& P, int p, int max_dept
 // through memory between bounces except the write-only bounce records.
 constexpr int kPathsBlock = 256;
 
-template <bool MEDIA, bool ALLFAM, int MINB>
+template <bool MEDIA, bool ALLFAM, int MINB, bool TIMED = false>
 __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathWork W) {
+  // TIMED (diagnostics): per-wave cycles in refill / world hit (mesh part) / record+scatter / fold
+  uint64_t tp[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t it = 0;
   SceneView S = S0;
   constexpr int TR = TR_BVH4_PRUNE | TR_WL;
   {
@@ -1622,6 +1627,9 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
     S.stris = (const DStandaloneTri*)(b + S0.world_off[4]);
     S.meshes = (const DMesh*)(b + S0.world_off[5]);
     S.media = (const DMedium*)(b + S0.world_off[6]);
+    S.mats = (const DMat*)(b + S0.world_off[7]);
+    S.texs = (const DTex*)(b + S0.world_off[8]);
+    S.lights = (const DLight*)(b + S0.world_off[9]);
   }
   __shared__ int s_node[kStack * kPathsBlock];
   __shared__ float s_t[kStack * kPathsBlock];
@@ -1635,6 +1643,7 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
   uint64_t spec = 0;
   uint32_t prays = 0, nrays = 0;
   for (;;) {
+    uint64_t tq = TIMED ? __builtin_amdgcn_s_memtime() : 0;
     // refill lanes whose path ended
     const bool need = g < 0 && !exhausted;
     const uint64_t nm = __ballot(need);
@@ -1664,14 +1673,34 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
       }
     }
     if (__ballot(g >= 0) == 0) break;
+    if (TIMED) {
+      __builtin_amdgcn_s_waitcnt(0);
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      tp[0] += t - tq;
+      tq = t;
+      cx.mesh_cycles = 0;
+      ++it;
+    }
     if (g >= 0) {
       ++prays;
-      const WorldHit w = world_hit<MEDIA, TR>(S, r, rng, cx);
+      const WorldHit w = world_hit<MEDIA, TIMED ? (TR_BVH4_TIMED | TR_WL) : TR>(S, r, rng, cx);
+      if (TIMED) {
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+        tp[1] += t - tq - cx.mesh_cycles;
+        tp[2] += cx.mesh_cycles;
+        tq = t;
+      }
       bool done = true;
       V3 C = v3(0.f);
       if (w.obj >= 0) {
         const HitRec h = world_record<TR>(S, r, w);
         const int kind = h.mat >= 0 ? S.mats[h.mat].kind : -1;
+        if (TIMED) {
+          __builtin_amdgcn_s_waitcnt(0);
+          const uint64_t t = __builtin_amdgcn_s_memtime();
+          tp[5] += t - tq;
+          tq = t;
+        }
         const int fam = family_of(h.mat, kind, depth, W.max_depth);
         if (fam == FAM_TERM) {
           C = hit_emitted(S, h.mat, r.d, h.p, h.n, h.u, h.v);
@@ -1691,6 +1720,11 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
           ++depth;
           done = false;
         }
+      }
+      if (TIMED) {
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+        tp[3] += t - tq;
+        tq = t;
       }
       if (done && (g >= W.n_paths || depth > W.max_depth)) {
         atomicOr(W.err, 4);
@@ -1721,7 +1755,13 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
         nrays += prays;
         g = -1;
       }
+      if (TIMED) tp[4] += __builtin_amdgcn_s_memtime() - tq;
     }
+  }
+  if (TIMED && lane_id() == 0) {  // per-wave totals -> W.counters[4..9]
+    for (int q = 0; q < 5; ++q) atomicAdd(W.counters + 4 + q, (unsigned long long)tp[q]);
+    atomicAdd(W.counters + 9, (unsigned long long)it);
+    atomicAdd(W.counters + 10, (unsigned long long)tp[5]);
   }
   unsigned long long tot = nrays;
   for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
@@ -2000,8 +2040,10 @@ int paths_lanes_per_device(const SceneView& S, int device) {
 
 void launch_paths(const SceneView& S, const PathWork& W, int all_families, hipStream_t st) {
   const int blocks = W.lanes / dev::kPathsBlock;
-#define SRR_LAUNCH_PATHS(M, A, B) \
-  hipLaunchKernelGGL((dev::k_paths<M, A, B>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W)
+  static const bool timed = getenv("SRR_PATHS_TIMING") != nullptr;
+#define SRR_LAUNCH_PATHS(M, A, B)                                                                      \
+  if (timed) hipLaunchKernelGGL((dev::k_paths<M, A, 4, true>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W); \
+  else hipLaunchKernelGGL((dev::k_paths<M, A, B>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W)
 #define SRR_LAUNCH_PATHS_B(M, A)                          \
   switch (paths_min_blocks()) {                           \
     case 2: SRR_LAUNCH_PATHS(M, A, 2); break;             \

@@ -65,7 +65,7 @@ int renderer_create(const Scene& sc, int device, srr_renderer** out, std::string
   RCHK(upload(&cm, cam, K));
   // world-traversal tables packed for LDS staging (kernels.h SceneView::world_blob)
   std::vector<uint8_t> blob;
-  int off[7];
+  int off[10];
   auto put = [&](int k, const void* data, size_t bytes) {
     off[k] = (int)blob.size();
     blob.insert(blob.end(), (const uint8_t*)data, (const uint8_t*)data + bytes);
@@ -78,12 +78,15 @@ int renderer_create(const Scene& sc, int device, srr_renderer** out, std::string
   put(4, F.stris.data(), F.stris.size() * sizeof(DStandaloneTri));
   put(5, F.meshes.data(), F.meshes.size() * sizeof(DMesh));
   put(6, F.media.data(), F.media.size() * sizeof(DMedium));
+  put(7, F.mats.data(), F.mats.size() * sizeof(DMat));
+  put(8, F.texs.data(), F.texs.size() * sizeof(DTex));
+  put(9, F.lights.data(), F.lights.size() * sizeof(DLight));
   uint8_t* wb;
   RCHK(upload(&wb, blob, K));
   SceneView& V = r->view;
   V.world_blob = (const uint4*)wb;
   V.world_words = (int)(blob.size() / 16);
-  for (int k = 0; k < 7; ++k) V.world_off[k] = off[k];
+  for (int k = 0; k < 10; ++k) V.world_off[k] = off[k];
   V.objs = objs;
   V.n_world = F.n_world;
   V.has_media = F.media.empty() ? 0 : 1;
@@ -240,8 +243,8 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
     RCHK(hipMalloc((void**)&r->pw_sample, win_paths * 3 * sizeof(float)));
     r->pw_sample_cap = win_paths;
   }
-  if (!r->pw_ctr) RCHK(hipMalloc((void**)&r->pw_ctr, 3 * sizeof(unsigned long long)));
-  RCHK(hipMemsetAsync(r->pw_ctr, 0, 3 * sizeof(unsigned long long), st));
+  if (!r->pw_ctr) RCHK(hipMalloc((void**)&r->pw_ctr, 16 * sizeof(unsigned long long)));
+  RCHK(hipMemsetAsync(r->pw_ctr, 0, 16 * sizeof(unsigned long long), st));
   RCHK(hipMemsetAsync(r->acc, 0, 3 * npix * sizeof(float), st));
   const bool all_fam = !r->diffuse_only;
   RCHK(hipEventRecord(r->ev_beg, st));
@@ -284,8 +287,13 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
   RCHK(hipEventRecord(r->ev_end, st));
   RCHK(hipStreamSynchronize(st));
   RCHK(hipGetLastError());
-  unsigned long long ctr[3] = {0, 0, 0};
+  unsigned long long ctr[16] = {0};
   RCHK(hipMemcpy(ctr, r->pw_ctr, sizeof(ctr), hipMemcpyDeviceToHost));
+  if (getenv("SRR_PATHS_TIMING") && ctr[9]) {
+    const double it = (double)ctr[9];
+    fprintf(stderr, "k_paths per wave-iteration (ticks): refill %.0f  world %.0f  mesh %.0f  record %.0f  scatter %.0f  fold %.0f  (%llu wave-iterations)\n",
+            ctr[4] / it, ctr[5] / it, ctr[6] / it, ctr[10] / it, (ctr[7] - ctr[10]) / it, ctr[8] / it, ctr[9]);
+  }
   const unsigned long long rays = ctr[0];
   if (ctr[2]) {
     err = "k_paths index guard tripped (bits " + std::to_string(ctr[2]) + ")";
