@@ -215,6 +215,8 @@ struct TraceCtx {
   unsigned long long* ctr;  // optional counters: boxes tested, triangle tests, stack overflows
   int* st_node;    // this thread's LDS stack (stride kTraceBlock)
   float* st_t;     // entry distance of each stacked node
+  const __attribute__((address_space(3))) f32x4* lds_nodes = nullptr;  // LDS copy of node4[0, lds_count) (k_paths)
+  int lds_count = 0;
   // SRR_TIMING diagnostics (wave-uniform): cycles inside mesh traversals, steps
   mutable uint64_t mesh_cycles = 0;
   mutable int mesh_steps = 0;
@@ -248,9 +250,19 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
   uint32_t nbox = 0, ntri = 0;
   const uint64_t tm_enter = TIMING ? __builtin_amdgcn_s_memtime() : 0;
   for (;;) {
-    const float4* N = S.node4 + 8 * (size_t)node;
-    const float4 LX = N[0], LY = N[1], LZ = N[2], HX = N[3], HY = N[4], HZ = N[5];
-    const int4 CH = *(const int4*)(N + 6);
+    float4 LX, LY, LZ, HX, HY, HZ;
+    int4 CH;
+    if (node < cx.lds_count) {  // top levels: LDS copy (k_paths)
+      const __attribute__((address_space(3))) f32x4* N = cx.lds_nodes + 8 * node;
+      auto f4 = [](f32x4 v) { return make_float4(v[0], v[1], v[2], v[3]); };
+      LX = f4(N[0]), LY = f4(N[1]), LZ = f4(N[2]), HX = f4(N[3]), HY = f4(N[4]), HZ = f4(N[5]);
+      const f32x4 c4 = N[6];
+      CH = make_int4(__float_as_int(c4[0]), __float_as_int(c4[1]), __float_as_int(c4[2]), __float_as_int(c4[3]));
+    } else {
+      const float4* N = S.node4 + 8 * (size_t)node;
+      LX = N[0], LY = N[1], LZ = N[2], HX = N[3], HY = N[4], HZ = N[5];
+      CH = *(const int4*)(N + 6);
+    }
     nbox += 4;
     float near[4];
     bool hit[4];
@@ -1633,7 +1645,12 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
   }
   __shared__ int s_node[kStack * kPathsBlock];
   __shared__ float s_t[kStack * kPathsBlock];
+  __shared__ float4 s_n4[kPathsLdsNodes * 8];
+  for (int i = threadIdx.x; i < S0.node4_lds * 8; i += blockDim.x) s_n4[i] = S0.node4[i];
+  __syncthreads();
   TraceCtx cx{nullptr, s_node + threadIdx.x, s_t + threadIdx.x};
+  cx.lds_nodes = (const __attribute__((address_space(3))) f32x4*)s_n4;
+  cx.lds_count = S0.node4_lds;
   const int slot = blockIdx.x * blockDim.x + threadIdx.x;
   long long g = -1;  // path of this lane, -1 idle
   bool exhausted = false;

@@ -97,6 +97,7 @@ int renderer_create(const Scene& sc, int device, srr_renderer** out, std::string
   V.meshes = me;
   V.nodes = (const float4*)nodes;
   V.node4 = (const float4*)n4;
+  V.node4_lds = (int)std::min<size_t>(kPathsLdsNodes, F.node4.size() / 32);
   V.tri_pos = (const float4*)tp;
   V.tri_shade = ts;
   V.media = md;

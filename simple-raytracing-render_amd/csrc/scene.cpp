@@ -757,6 +757,26 @@ struct Flattener {
     };
     build(0);
     m.n_node4 = (int)(F.node4.size() / 32) - m.node4_off;
+    // breadth-first layout: the top levels come first, so the path kernel can
+    // keep a prefix of the array in LDS (SceneView::node4_lds)
+    std::vector<int> order{m.node4_off}, newidx(F.node4.size() / 32, -1);
+    for (size_t i = 0; i < order.size(); ++i) {
+      newidx[order[i]] = m.node4_off + (int)i;
+      int32_t ch[4];
+      std::memcpy(ch, &F.node4[32 * (size_t)order[i] + 24], 16);
+      for (int c = 0; c < 4; ++c)
+        if (ch[c] >= 0) order.push_back(ch[c]);
+    }
+    std::vector<float> bfs(32 * order.size());
+    for (size_t i = 0; i < order.size(); ++i) {
+      std::memcpy(&bfs[32 * i], &F.node4[32 * (size_t)order[i]], 32 * sizeof(float));
+      int32_t ch[4];
+      std::memcpy(ch, &bfs[32 * i + 24], 16);
+      for (int c = 0; c < 4; ++c)
+        if (ch[c] >= 0) ch[c] = newidx[ch[c]];
+      std::memcpy(&bfs[32 * i + 24], ch, 16);
+    }
+    std::copy(bfs.begin(), bfs.end(), F.node4.begin() + 32 * (size_t)m.node4_off);
   }
 
   int add_mesh(int h) {  // a bvh_node whose leaves are all bare triangles
