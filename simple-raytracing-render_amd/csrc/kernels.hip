@@ -1619,6 +1619,7 @@ SRR_D bool shade_one(const SceneView& S, const PathState& P, int p, int max_dept
 // a global cursor (one wave-aggregated atomic per refill).  No path state goes
 // through memory between bounces except the write-only bounce records.
 constexpr int kPathsBlock = 256;
+constexpr unsigned long long kPoolChunk = 64;  // path indices a wave takes per cursor atomic
 
 template <bool MEDIA, bool ALLFAM, int MINB, bool TIMED = false>
 __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathWork W) {
@@ -1654,6 +1655,9 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
   const int slot = blockIdx.x * blockDim.x + threadIdx.x;
   long long g = -1;  // path of this lane, -1 idle
   bool exhausted = false;
+  unsigned long long pool = 0, pool_end = 0;  // the wave's unissued path indices [pool, pool_end)
+  unsigned long long nxt_lane0 = 0;           // lane 0: base of the armed next chunk
+  bool nxt_armed = false;
   Ray r{};
   Rng rng{};
   int depth = 0;
@@ -1661,16 +1665,34 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
   uint32_t prays = 0, nrays = 0;
   for (;;) {
     uint64_t tq = TIMED ? __builtin_amdgcn_s_memtime() : 0;
-    // refill lanes whose path ended
+    // refill lanes whose path ended, from the wave's pool of path indices; the
+    // pool is re-armed one chunk ahead (an atomic whose result is first read an
+    // iteration later, so its latency hides behind that iteration's work)
     const bool need = g < 0 && !exhausted;
     const uint64_t nm = __ballot(need);
     if (nm) {
-      const int leader = __ffsll((unsigned long long)nm) - 1;
-      unsigned long long base = 0;
-      if (lane_id() == leader) base = atomicAdd(W.cursor, (unsigned long long)__popcll(nm));
-      base = __shfl(base, leader);
+      const unsigned long long cnt = __popcll(nm);
+      const unsigned long long rank = __popcll(nm & ((1ull << lane_id()) - 1));
+      unsigned long long avail = pool_end - pool;
+      long long idx;
+      if (avail >= cnt) {
+        idx = (long long)(pool + rank);
+        pool += cnt;
+      } else {
+        unsigned long long nb;
+        if (nxt_armed) {
+          nb = __shfl(nxt_lane0, 0);
+          nxt_armed = false;
+        } else {
+          unsigned long long b = 0;
+          if (lane_id() == 0) b = atomicAdd(W.cursor, (unsigned long long)kPoolChunk);
+          nb = __shfl(b, 0);
+        }
+        idx = (long long)(rank < avail ? pool + rank : nb + (rank - avail));
+        pool = nb + (cnt - avail);
+        pool_end = nb + kPoolChunk;
+      }
       if (need) {
-        const long long idx = (long long)base + __popcll(nm & ((1ull << lane_id()) - 1));
         if (idx < W.n_paths) {
           g = idx;
           const int lp = (int)(idx / W.spp_w), s = (int)(idx % W.spp_w);  // pixel-major: g = lp * spp_w + s
@@ -1688,6 +1710,10 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
           exhausted = true;
         }
       }
+    }
+    if (!nxt_armed && pool_end < (unsigned long long)W.n_paths) {  // arm the next chunk
+      if (lane_id() == 0) nxt_lane0 = atomicAdd(W.cursor, (unsigned long long)kPoolChunk);
+      nxt_armed = true;
     }
     if (__ballot(g >= 0) == 0) break;
     if (TIMED) {
