@@ -13,11 +13,12 @@ from srr import capi, scenes
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIBDIR = os.path.join(ROOT, "simple-raytracing-render_amd")
 SRC = os.path.join(ROOT, "tests", "cpp", "cornell_teapot.cpp")
+REF_API_SRC = os.path.join(ROOT, "tests", "cpp", "ref_api_cornell.cpp")
 
 
-def build(tmpdir):
-    exe = os.path.join(str(tmpdir), "cornell_teapot")
-    subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), SRC,
+def build(tmpdir, src=SRC, name="cornell_teapot"):
+    exe = os.path.join(str(tmpdir), name)
+    subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), src,
                     "-o", exe, "-L", LIBDIR, "-lsrr", f"-Wl,-rpath,{LIBDIR}"], check=True)
     return exe
 
@@ -40,3 +41,23 @@ def test_example_renders_the_python_built_scene(tmp_path):
     np.testing.assert_array_equal(got.view(np.uint32), want["mean"].view(np.uint32))
     head = open(ppm, "rb").read(32).split(b"\n")
     assert head[0] == b"P3" and head[1].split() == [str(nx).encode(), str(ny).encode()]
+
+
+def test_reference_style_builder_compiles(tmp_path):
+    """include/srr/ref_api.h: a builder in the reference's own style (new sphere,
+    new bvh_node(list, n, 0, 1), teapot::createPloyTeapot, camera) compiles."""
+    exe = build(tmp_path, REF_API_SRC, "ref_api_cornell")
+    out = subprocess.run([exe], capture_output=True, text=True)
+    assert out.returncode == 2 and "usage" in out.stderr
+
+
+@pytest.mark.gpu
+def test_reference_style_builder_renders_the_python_built_scene(tmp_path):
+    exe = build(tmp_path, REF_API_SRC, "ref_api_cornell")
+    nx, ny, spp = 40, 24, 4
+    meanf = str(tmp_path / "m.f32")
+    subprocess.run([exe, str(nx), str(ny), str(spp), meanf], check=True, timeout=300)
+    got = np.fromfile(meanf, np.float32).reshape(nx * ny, 3)
+    sc, _ = scenes.s2_cornell_teapot()
+    want = capi.Renderer(sc.text()).render(nx, ny, spp, 50)
+    np.testing.assert_array_equal(got.view(np.uint32), want["mean"].view(np.uint32))
