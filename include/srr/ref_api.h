@@ -268,6 +268,25 @@ class teapot {
   int count_ = 0;
 };
 
+/* model.h:13-102 (assimp replaced by srr's PLY / binary-FBX loader, srr_model):
+ * the file is read in the constructor; genhitablemodel() and gettrianglecount()
+ * cover mesh 0 only, as the reference's do (model.h:90, :101). */
+class model {
+ public:
+  model(const std::string& filename, bool flipUVs, bool flipWindingOrder, material* mat, vec3 scale) {
+    count_ = check(srr_model(cur(), filename.c_str(), flipUVs, flipWindingOrder, mat_handle(mat), scale.e, &first_));
+  }
+  hitable** genhitablemodel() {
+    hitable** list = new hitable*[(size_t)count_];
+    for (int k = 0; k < count_; ++k) list[k] = new triangle(first_ + k);
+    return list;
+  }
+  int gettrianglecount() const { return count_; }
+
+ private:
+  int first_ = 0, count_ = 0;
+};
+
 /* camera.h:19-48 */
 class camera {
  public:

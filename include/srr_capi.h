@@ -104,6 +104,21 @@ int srr_bvh_node(srr_scene* s, const int* children, int n, float time0, float ti
  * triangle handles, first_handle .. first_handle+count-1, returns count. */
 int srr_teapot(srr_scene* s, float scale, int divs, int mat, int* first_handle);
 
+/* model.h:27-102 (assimp replaced by srr's PLY / binary-FBX readers): the file's
+ * first mesh (model::genhitablemodel returns mesh 0 only) as triangles built like
+ * geometry.h:55-77: positions scaled per component, UV channel 0 (v -> 1 - v with
+ * flip_uvs), index order reversed with flip_winding, polygons fanned.  Creates
+ * count triangle handles first_handle .. first_handle+count-1 and returns count.
+ * Files without normals get face normals (SURVEY Q19 build definition). */
+int srr_model(srr_scene* s, const char* path, int flip_uvs, int flip_winding, int mat, const float scale[3],
+              int* first_handle);
+/* The same triangles without a scene: per triangle 9 floats each of positions,
+ * uvs (u, v, 0 per corner) and normals (zeros when the file has none; the scene
+ * then uses face normals).  Buffers may be NULL to ask for the count.
+ * flags_out (may be NULL): bit 0 file has normals, bit 1 file has UVs. */
+int srr_mesh_file_triangles(const char* path, int flip_uvs, int flip_winding, const float scale[3], float* pos9,
+                            float* uv9, float* nrm9, int* flags_out);
+
 /* camera.h:33-48, 9-argument constructor */
 int srr_camera(srr_scene* s, const float lookfrom[3], const float lookat[3], const float vup[3], float vfov,
                float aspect, float aperture, float focus_dist, float t0, float t1);

@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "../../include/srr_capi.h"
+#include "meshio.h"
 #include "renderer.h"
 
 using namespace srr;
@@ -344,6 +345,49 @@ int srr_tonemap(const float* mean, int64_t n, unsigned char* rgb8) {  // Raytrac
     rgb8[i] = (unsigned char)q;
   }
   return 0;
+}
+
+int srr_mesh_file_triangles(const char* path, int flip_uvs, int flip_winding, const float scale[3], float* pos9,
+                            float* uv9, float* nrm9, int* flags_out) {
+  if (!path || !scale) return fail(SRR_EINVAL, "null argument");
+  srr::MeshData m;
+  std::string err;
+  if (srr::load_mesh_file(path, m, err) < 0) return fail(SRR_EIO, err);
+  srr::apply_model_semantics(m, flip_uvs != 0, flip_winding != 0, scale);
+  for (size_t t = 0; t < m.tris.size(); ++t)
+    for (int j = 0; j < 3; ++j) {
+      const srr::MeshData::Corner& c = m.tris[t][j];
+      if (pos9) std::memcpy(pos9 + 9 * t + 3 * j, c.p, 12);
+      if (uv9) std::memcpy(uv9 + 9 * t + 3 * j, c.uv, 12);
+      if (nrm9) std::memcpy(nrm9 + 9 * t + 3 * j, c.n, 12);
+    }
+  if (flags_out) *flags_out = (m.has_normals ? 1 : 0) | (m.has_uvs ? 2 : 0);
+  if (m.tris.size() > (size_t)INT32_MAX / 2) return fail(SRR_EINVAL, "mesh too large");
+  return (int)m.tris.size();
+}
+
+int srr_model(srr_scene* s, const char* path, int flip_uvs, int flip_winding, int mat, const float scale[3],
+              int* first_handle) {
+  if (!s || !path || !scale) return fail(SRR_EINVAL, "null argument");
+  srr::MeshData m;
+  std::string err;
+  if (srr::load_mesh_file(path, m, err) < 0) return fail(SRR_EIO, err);
+  srr::apply_model_semantics(m, flip_uvs != 0, flip_winding != 0, scale);
+  if (m.tris.empty()) return fail(SRR_EINVAL, std::string(path) + ": mesh 0 has no triangles");
+  int first = -1;
+  for (const auto& t : m.tris) {
+    float p[9], uv[9], n[9];
+    for (int j = 0; j < 3; ++j) {
+      std::memcpy(p + 3 * j, t[j].p, 12);
+      std::memcpy(uv + 3 * j, t[j].uv, 12);
+      std::memcpy(n + 3 * j, t[j].n, 12);
+    }
+    int h = srr_triangle(s, p, mat, uv, m.has_normals ? n : nullptr);
+    if (h < 0) return h;
+    if (first < 0) first = h;
+  }
+  if (first_handle) *first_handle = first;
+  return (int)m.tris.size();
 }
 
 int srr_write_ppm(const char* path, int nx, int ny, const unsigned char* rgb8) {

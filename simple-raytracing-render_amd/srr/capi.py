@@ -61,6 +61,7 @@ def lib():
         L.srr_tonemap.argtypes = [vp, ctypes.c_int64, vp]
         L.srr_write_ppm.argtypes = [cp, ip, ip, vp]
         L.srr_sobol_points.argtypes = [ip, vp]
+        L.srr_mesh_file_triangles.argtypes = [cp, ip, ip, vp, vp, vp, vp, ctypes.POINTER(ip)]
         _LIB = L
     return _LIB
 
@@ -158,3 +159,17 @@ def tonemap(mean: np.ndarray) -> np.ndarray:
 def write_ppm(path: str, nx: int, ny: int, img8: np.ndarray) -> None:
     img8 = np.ascontiguousarray(img8, np.uint8)
     _check(lib().srr_write_ppm(path.encode(), nx, ny, _ptr(img8)))
+
+
+def mesh_file_triangles(path: str, flip_uvs: bool = False, flip_winding: bool = False, scale=(1.0, 1.0, 1.0)):
+    """Mesh 0 of a PLY / binary FBX file as the reference's model loader builds it
+    (model.h:28-59, geometry.h:24-79): returns ``(pos, uv, nrm, has_normals,
+    has_uvs)`` with arrays of shape (n_tris, 3 corners, 3)."""
+    sc = np.ascontiguousarray(scale, np.float32)
+    fl = ctypes.c_int(0)
+    n = _check(lib().srr_mesh_file_triangles(path.encode(), int(flip_uvs), int(flip_winding), _ptr(sc), None, None,
+                                             None, ctypes.byref(fl)))
+    pos, uv, nrm = (np.zeros((n, 3, 3), np.float32) for _ in range(3))
+    _check(lib().srr_mesh_file_triangles(path.encode(), int(flip_uvs), int(flip_winding), _ptr(sc), _ptr(pos),
+                                         _ptr(uv), _ptr(nrm), None))
+    return pos, uv, nrm, bool(fl.value & 1), bool(fl.value & 2)

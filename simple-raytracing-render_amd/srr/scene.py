@@ -213,6 +213,22 @@ class Scene:
         self._emit("grp", g.id, "teapot", f32(scale), int(divs), mat.id)
         return g
 
+    def model(self, filename: str, flip_uvs: bool, flip_winding: bool, mat: Mat = NULL_MAT,
+              scale=(1.0, 1.0, 1.0)) -> list[Obj]:
+        """``model(filename, flipUVs, flipWindingOrder, mat, scale).genhitablemodel()``
+        (model.h:28-59, :75-91; geometry.h:24-90): the triangles of the file's first
+        mesh, read now by srr's PLY / binary-FBX loader (assimp replaced) and
+        recorded as explicit triangles, so every consumer of the text sees the same
+        vertices.  Triangles carry the file's normals when it has them, else their
+        face normal (SURVEY Q19 build definition); corners without UVs get (0,0,0)."""
+        from .capi import mesh_file_triangles  # the loader lives in libsrr
+        pos, uv, nrm, has_n, _ = mesh_file_triangles(filename, flip_uvs, flip_winding, scale)
+        out = []
+        for t in range(len(pos)):
+            out.append(self.triangle(*pos[t].tolist(), mat=mat, uvs=uv[t].tolist(),
+                                     normals=nrm[t].tolist() if has_n else None))
+        return out
+
     # -------------------------------------------------------------- camera
     def camera(self, lookfrom, lookat, vup, vfov, aspect, aperture, focus_dist, t0=0.0, t1=1.0) -> None:
         self._emit("camera", *self._v(lookfrom), *self._v(lookat), *self._v(vup), f32(vfov), f32(aspect),

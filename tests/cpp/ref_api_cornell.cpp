@@ -5,7 +5,10 @@
 // through the C-ABI.  tests/test_integration_example.py checks its image against
 // the Python-built S2 scene bitwise.
 //
-//   ref_api_cornell NX NY SPP OUT_MEAN.f32
+//   ref_api_cornell NX NY SPP OUT_MEAN.f32 [MESH_FILE]
+//
+// With MESH_FILE the teapot is replaced by model(MESH_FILE, ...).genhitablemodel()
+// (model.h:28-91), the way the reference's soldier_scene loads its mesh.
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -13,6 +16,8 @@
 #include "srr/ref_api.h"
 
 using namespace srr::ref;
+
+static const char* g_mesh = nullptr;
 
 void cornell_teapot(hitable** scene, camera** cam, hitable** hlist, float aspect) {
   int i = 0;
@@ -28,9 +33,18 @@ void cornell_teapot(hitable** scene, camera** cam, hitable** hlist, float aspect
   list[i++] = new flip_normals(new xy_rect(0, 555, 0, 555, 555, white));
   list[i++] = new flip_normals(new xz_rect(213, 343, 227, 332, 554, light));
   list[i++] = new sphere(vec3(190, 90, 190), 90, white);
-  teapot* tp = new teapot(60, white, 10);
-  hitable** tris = tp->createPloyTeapot();
-  list[i++] = new translate(new rotate_x(new bvh_node(tris, tp->getTriangleCount(), 0, 1), 90), vec3(330, 0, 300));
+  hitable** tris;
+  int ntris;
+  if (g_mesh) {
+    model* m = new model(g_mesh, true, true, white, vec3(1, 1, 1));
+    tris = m->genhitablemodel();
+    ntris = m->gettrianglecount();
+  } else {
+    teapot* tp = new teapot(60, white, 10);
+    tris = tp->createPloyTeapot();
+    ntris = tp->getTriangleCount();
+  }
+  list[i++] = new translate(new rotate_x(new bvh_node(tris, ntris, 0, 1), 90), vec3(330, 0, 300));
   *scene = new hitable_list(list, i);
   *cam = new camera(vec3(278, 278, -800), vec3(278, 278, 0), vec3(0, 1, 0), 40, aspect, 0.0f, 10.0f, 0.0f, 1.0f);
   hitable** lights = new hitable*[1];
@@ -40,9 +54,10 @@ void cornell_teapot(hitable** scene, camera** cam, hitable** hlist, float aspect
 
 int main(int argc, char** argv) {
   if (argc < 5) {
-    std::fprintf(stderr, "usage: %s NX NY SPP OUT_MEAN.f32\n", argv[0]);
+    std::fprintf(stderr, "usage: %s NX NY SPP OUT_MEAN.f32 [MESH_FILE]\n", argv[0]);
     return 2;
   }
+  if (argc > 5) g_mesh = argv[5];
   srr_scene* s = srr_scene_create();
   hitable *world = nullptr, *hlist = nullptr;
   camera* cam = nullptr;

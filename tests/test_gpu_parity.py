@@ -153,3 +153,33 @@ def test_depth_limit_zero_and_one():
         ref = ob.render(text, 16, 16, 4, md)
         pc = parity.compare_paths(out["paths"], ref["paths"])
         assert pc["match"] >= parity.MIN_MATCH, (md, pc)
+
+
+def test_model_file_scene_matches_oracle(tmp_path):
+    """A mesh read from a file (model.h path): the teapot written
+    as a binary PLY with per-vertex normals and UVs, loaded through Scene.model
+    (srr's PLY loader), rendered on the GPU and by the oracle from the same text."""
+    import meshfiles as mf
+    from srr.scene import Scene
+    tp = ob.teapot(60.0, 6).reshape(-1, 12)
+    n_t = len(tp)
+    verts = tp[:, :9].reshape(-1, 3)
+    rng = np.random.default_rng(11)
+    nrm = np.repeat(tp[:, 9:12], 3, axis=0) + 0.2 * rng.standard_normal((3 * n_t, 3)).astype(np.float32)
+    uvs = rng.random((3 * n_t, 2)).astype(np.float32)
+    path = str(tmp_path / "teapot.ply")
+    mf.write_ply(path, verts, [[3 * t, 3 * t + 1, 3 * t + 2] for t in range(n_t)], nrm, uvs,
+                 fmt="binary_little_endian")
+    sc = Scene()
+    objs, white = scenes._cornell(sc)
+    tris = sc.model(path, True, True, white, (1.0, 1.0, 1.0))
+    objs.append(sc.translate(sc.rotate_x(sc.bvh_node(tris, 0, 1), 90), (330, 0, 300)))
+    sc.set_world(sc.hitable_list(objs))
+    scenes._cornell_camera_and_lights(sc)
+    text = sc.text()
+    nx, ny, spp = 32, 32, 8
+    out = capi.Renderer(text).render(nx, ny, spp, 50, keep_paths=True)
+    ref = ob.render(text, nx, ny, spp, 50, threads=8)
+    pc = parity.compare_paths(out["paths"], ref["paths"])
+    print("model scene:", pc)
+    assert pc["match"] >= parity.MIN_MATCH, pc

@@ -61,3 +61,31 @@ def test_reference_style_builder_renders_the_python_built_scene(tmp_path):
     sc, _ = scenes.s2_cornell_teapot()
     want = capi.Renderer(sc.text()).render(nx, ny, spp, 50)
     np.testing.assert_array_equal(got.view(np.uint32), want["mean"].view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_reference_style_model_loader_renders_the_python_built_scene(tmp_path):
+    """model(file, flipUVs, flipWindingOrder, mat, scale).genhitablemodel() from
+    C++ (include/srr/ref_api.h -> srr_model) and Scene.model from Python read the
+    same PLY file and give bitwise the same image."""
+    import meshfiles as mf
+    import oracle_bind as ob
+    exe = build(tmp_path, REF_API_SRC, "ref_api_cornell")
+    tp = ob.teapot(60.0, 6).reshape(-1, 12)
+    n_t = len(tp)
+    path = str(tmp_path / "teapot.ply")
+    mf.write_ply(path, tp[:, :9].reshape(-1, 3), [[3 * t, 3 * t + 1, 3 * t + 2] for t in range(n_t)],
+                 np.repeat(tp[:, 9:12], 3, axis=0), np.zeros((3 * n_t, 2), np.float32), fmt="binary_little_endian")
+    nx, ny, spp = 40, 24, 4
+    meanf = str(tmp_path / "m.f32")
+    subprocess.run([exe, str(nx), str(ny), str(spp), meanf, path], check=True, timeout=300)
+    got = np.fromfile(meanf, np.float32).reshape(nx * ny, 3)
+    from srr.scene import Scene
+    sc = Scene()
+    objs, white = scenes._cornell(sc)
+    tris = sc.model(path, True, True, white, (1.0, 1.0, 1.0))
+    objs.append(sc.translate(sc.rotate_x(sc.bvh_node(tris, 0, 1), 90), (330, 0, 300)))
+    sc.set_world(sc.hitable_list(objs))
+    scenes._cornell_camera_and_lights(sc)
+    want = capi.Renderer(sc.text()).render(nx, ny, spp, 50)
+    np.testing.assert_array_equal(got.view(np.uint32), want["mean"].view(np.uint32))
