@@ -61,6 +61,11 @@ int srr_constant_texture(srr_scene* s, float r, float g, float b);
 /* texture.h:48-70 image_texture(unsigned char* pixels, int nx, int ny): RGB8,
  * row 0 = top; the bytes are copied (the reference borrows them). */
 int srr_image_texture(srr_scene* s, const unsigned char* rgb, int nx, int ny);
+/* image_texture(stbi_load(path, &tx, &ty, &tn, 0), tx, ty), the builders' idiom
+ * (Raytracing_n.cpp:269-270, :614-616, :631-632): decodes PNG / baseline JPEG /
+ * TGA as stb_image v2.19 does (byte-identical, tests/test_imageio.py) and keeps
+ * the 3 bytes per texel image_texture addresses. */
+int srr_image_texture_file(srr_scene* s, const char* path);
 /* Synthetic RGB8 image (stand-in for stbi_load'ed assets; kind 0 sky, 1 wood,
  * 2 checker), identical bytes on every consumer. */
 int srr_image_texture_gen(srr_scene* s, int nx, int ny, uint32_t seed, int kind);
@@ -184,6 +189,15 @@ int srr_copy_paths(srr_renderer* r, float* radiance, unsigned char* rays);
 int srr_tonemap(const float* mean, int64_t n_pixels, unsigned char* rgb8);
 /* Write an ASCII P3 PPM (Raytracing_n.cpp:886, 873-876). */
 int srr_write_ppm(const char* path, int nx, int ny, const unsigned char* rgb8);
+
+/* PNG (8-bit RGB) of the tone-mapped image -- the output option next to PPM. */
+int srr_write_png(const char* path, int nx, int ny, const unsigned char* rgb8);
+/* stbi_load(path, x, y, comp, req_comp) (stb_image.h v2.19, used throughout
+ * Raytracing_n.cpp): PNG, baseline JPEG, TGA.  *comp = the file's channels;
+ * returns the channels in *out (req_comp, or *comp when req_comp is 0) or a
+ * negative code.  Free *out with srr_image_free. */
+int srr_image_load(const char* path, int req_comp, int* x, int* y, int* comp, unsigned char** out);
+void srr_image_free(unsigned char* pixels);
 
 /* Sobol (0,2)-points of Raytracing_n.cpp:721-812, out[n][2]. */
 int srr_sobol_points(int n, double* out);

@@ -15,6 +15,7 @@
 //   teapot <scale> <divs> <out.f32>                tessellated vertices
 //   sobol  <N> <out.f64>
 //   kat    <name> <n> <seed> <out.bin>             per-function known answers
+//   image  <file> <req_comp> <out.raw>             stbi_load (stb_image v2.19)
 #define private public
 #define main ref_main
 #include "Raytracing_n.cpp"
@@ -97,6 +98,11 @@ RefScene build(const std::vector<Cmd>& cmds) {
       else if (t == "image_gen") {
         int w = (int)c.i(3), h = (int)c.i(4);
         auto* px = new std::vector<unsigned char>(srr_text::gen_image(w, h, (unsigned)c.u(5), (int)c.i(6)));
+        S.images.push_back(px);
+        S.tex[id] = new image_texture(px->data(), w, h);
+      } else if (t == "image_raw") {
+        int w = (int)c.i(3), h = (int)c.i(4);
+        auto* px = new std::vector<unsigned char>(srr_text::read_raw_image(c.at(5), w, h));
         S.images.push_back(px);
         S.tex[id] = new image_texture(px->data(), w, h);
       } else if (t == "checker") S.tex[id] = new checker_texture(S.tex.at(c.i(3)), S.tex.at(c.i(4)));
@@ -370,6 +376,23 @@ int cmd_teapot_data(int argc, char** argv) {
   return 0;
 }
 
+// image <file> <req_comp> <out.raw>: the reference's own stbi_load (stb_image
+// v2.19 compiled inside Raytracing_n.cpp), decoded bytes to out.raw; prints
+// "x y comp".
+int cmd_image(int argc, char** argv) {
+  if (argc < 5) return 2;
+  int x = 0, y = 0, n = 0, req = atoi(argv[3]);
+  unsigned char* px = stbi_load(argv[2], &x, &y, &n, req);
+  if (!px) {
+    fprintf(stderr, "stbi_load failed: %s\n", stbi_failure_reason());
+    return 1;
+  }
+  write(argv[4], px, (size_t)x * y * (req ? req : n));
+  stbi_image_free(px);
+  printf("%d %d %d\n", x, y, n);
+  return 0;
+}
+
 int cmd_kat(int argc, char** argv);
 
 }  // namespace
@@ -388,6 +411,7 @@ int main(int argc, char** argv) {
     if (c == "teapot") return cmd_teapot(argc, argv);
     if (c == "sobol") return cmd_sobol(argc, argv);
     if (c == "kat") return cmd_kat(argc, argv);
+    if (c == "image") return cmd_image(argc, argv);
     if (c == "teapot_data") return cmd_teapot_data(argc, argv);
   } catch (const std::exception& e) {
     fprintf(stderr, "ref_harness: %s\n", e.what());

@@ -1288,6 +1288,12 @@ std::unique_ptr<Scene> build(const std::string& text) {
         im->ny = (int)c.i(4);
         im->px = srr_text::gen_image(im->nx, im->ny, (unsigned)c.u(5), (int)c.i(6));
         x = im;
+      } else if (t == "image_raw") {
+        auto* im = new ImageTex();
+        im->nx = (int)c.i(3);
+        im->ny = (int)c.i(4);
+        im->px = srr_text::read_raw_image(c.at(5), im->nx, im->ny);
+        x = im;
       } else if (t == "checker") {
         auto* ck = new CheckerTex();
         ck->even = S->tex.at(c.i(3));

@@ -80,6 +80,15 @@ inline unsigned long long path_seed(unsigned x, unsigned y, unsigned s, unsigned
   return h & 0xFFFFFFFFFFFFULL;
 }
 
+// `tex <id> image_raw w h path`: an already decoded RGB8 image, w*h*3 bytes,
+// row 0 = top (what stbi_load returns for the reference's RGB assets).
+inline std::vector<unsigned char> read_raw_image(const std::string& path, int w, int h) {
+  std::string b = read_file(path.c_str());
+  if (w <= 0 || h <= 0 || b.size() != (size_t)w * h * 3)
+    throw std::runtime_error("image_raw " + path + ": expected " + std::to_string((size_t)w * h * 3) + " bytes");
+  return std::vector<unsigned char>(b.begin(), b.end());
+}
+
 // Synthetic RGB8 images (`tex <id> image_gen w h seed kind`), integer-only so
 // every consumer produces identical bytes.  kind: 0 sky, 1 wood, 2 checker.
 inline unsigned hash32(unsigned a) {

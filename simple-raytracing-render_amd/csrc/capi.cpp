@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "../../include/srr_capi.h"
+#include "imageio.h"
 #include "meshio.h"
 #include "renderer.h"
 
@@ -103,6 +104,23 @@ int srr_image_texture(srr_scene* s, const unsigned char* rgb, int nx, int ny) {
   t.nx = nx;
   t.ny = ny;
   t.px.assign(rgb, rgb + (size_t)nx * ny * 3);
+  return s->s.add_tex(std::move(t));
+}
+int srr_image_texture_file(srr_scene* s, const char* path) {
+  SCN(s);
+  if (!path) return fail(SRR_EINVAL, "null path");
+  srr::Image im;
+  std::string err;
+  if (srr::load_image(path, 0, im, err) < 0) return fail(SRR_EIO, err);
+  // image_texture reads 3 bytes per texel from the buffer stbi_load returned,
+  // whatever its channel count (texture.h:58-70): keep exactly the
+  // bytes it can address.  Fewer than 3 channels would read past that buffer.
+  if (im.n < 3) return fail(SRR_EINVAL, std::string(path) + ": image_texture needs 3 or 4 channels");
+  HTex t;
+  t.kind = TEX_IMAGE;
+  t.nx = im.w;
+  t.ny = im.h;
+  t.px.assign(im.px.begin(), im.px.begin() + (size_t)im.w * im.h * 3);
   return s->s.add_tex(std::move(t));
 }
 int srr_image_texture_gen(srr_scene* s, int nx, int ny, uint32_t seed, int kind) {
@@ -398,6 +416,37 @@ int srr_write_ppm(const char* path, int nx, int ny, const unsigned char* rgb8) {
   fclose(f);
   return 0;
 }
+
+int srr_write_png(const char* path, int nx, int ny, const unsigned char* rgb8) {
+  if (!path || !rgb8) return fail(SRR_EINVAL, "null argument");
+  std::vector<uint8_t> png;
+  std::string err;
+  int rc = srr::encode_png(rgb8, nx, ny, 3, png, err);
+  if (rc < 0) return fail(rc, err);
+  FILE* f = fopen(path, "wb");
+  if (!f) return fail(SRR_EIO, std::string("cannot open ") + path);
+  size_t w = fwrite(png.data(), 1, png.size(), f);
+  fclose(f);
+  return w == png.size() ? 0 : fail(SRR_EIO, std::string("short write to ") + path);
+}
+
+int srr_image_load(const char* path, int req_comp, int* x, int* y, int* comp, unsigned char** out) {
+  if (!path || !x || !y || !out) return fail(SRR_EINVAL, "null argument");
+  *out = nullptr;
+  srr::Image im;
+  std::string err;
+  int rc = srr::load_image(path, req_comp, im, err);
+  if (rc < 0) return fail(rc == -2 ? SRR_EIO : SRR_EINVAL, err);
+  *x = im.w;
+  *y = im.h;
+  if (comp) *comp = im.file_n;
+  *out = (unsigned char*)malloc(im.px.size());
+  if (!*out) return fail(SRR_ENOMEM, "out of memory");
+  std::memcpy(*out, im.px.data(), im.px.size());
+  return im.n;
+}
+
+void srr_image_free(unsigned char* pixels) { free(pixels); }
 
 int srr_teapot_vertices(float scale, int divs, float* out) {
   if (divs < 1 || divs > 400) return fail(SRR_EINVAL, "teapot divs out of range");

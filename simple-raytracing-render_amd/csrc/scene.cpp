@@ -10,7 +10,9 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <fstream>
 #include <functional>
+#include <iterator>
 #include <map>
 #include <sstream>
 
@@ -1012,6 +1014,15 @@ int scene_from_text(const std::string& text, Scene& S, std::string& err) {
           x.nx = (int)c.i(3);
           x.ny = (int)c.i(4);
           x.px = gen_image(x.nx, x.ny, (uint32_t)c.u(5), (int)c.i(6));
+        } else if (t == "image_raw") {  // decoded RGB8 file, w*h*3 bytes, row 0 = top
+          x.kind = TEX_IMAGE;
+          x.nx = (int)c.i(3);
+          x.ny = (int)c.i(4);
+          std::ifstream f(c.t.at(5), std::ios::binary);
+          if (!f) throw std::runtime_error("image_raw: cannot open " + c.t.at(5));
+          x.px.assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
+          if (x.nx <= 0 || x.ny <= 0 || x.px.size() != (size_t)x.nx * x.ny * 3)
+            throw std::runtime_error("image_raw " + c.t.at(5) + ": size does not match " + c.t.at(3) + "x" + c.t.at(4));
         } else if (t == "checker") {
           x.kind = TEX_CHECKER;
           x.even = need(T, c.i(3), "tex");

@@ -62,6 +62,12 @@ def lib():
         L.srr_write_ppm.argtypes = [cp, ip, ip, vp]
         L.srr_sobol_points.argtypes = [ip, vp]
         L.srr_mesh_file_triangles.argtypes = [cp, ip, ip, vp, vp, vp, vp, ctypes.POINTER(ip)]
+        u8p = ctypes.POINTER(ctypes.c_ubyte)
+        L.srr_image_load.argtypes = [cp, ip, ctypes.POINTER(ip), ctypes.POINTER(ip), ctypes.POINTER(ip),
+                                     ctypes.POINTER(u8p)]
+        L.srr_image_free.argtypes = [u8p]
+        L.srr_image_free.restype = None
+        L.srr_write_png.argtypes = [cp, ip, ip, vp]
         _LIB = L
     return _LIB
 
@@ -159,6 +165,28 @@ def tonemap(mean: np.ndarray) -> np.ndarray:
 def write_ppm(path: str, nx: int, ny: int, img8: np.ndarray) -> None:
     img8 = np.ascontiguousarray(img8, np.uint8)
     _check(lib().srr_write_ppm(path.encode(), nx, ny, _ptr(img8)))
+
+
+def image_load(path: str, req_comp: int = 0) -> tuple[np.ndarray, int]:
+    """stbi_load(path, &x, &y, &comp, req_comp) (stb_image v2.19, as the
+    reference's builders call it): returns ``(pixels[y, x, channels], comp)``
+    with comp the file's own channel count."""
+    x, y, n = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    p = ctypes.POINTER(ctypes.c_ubyte)()
+    ch = _check(lib().srr_image_load(path.encode(), req_comp, ctypes.byref(x), ctypes.byref(y), ctypes.byref(n),
+                                     ctypes.byref(p)))
+    try:
+        px = np.ctypeslib.as_array(p, shape=(y.value, x.value, ch)).copy()
+    finally:
+        lib().srr_image_free(p)
+    return px, n.value
+
+
+def write_png(path: str, nx: int, ny: int, img8: np.ndarray) -> None:
+    img8 = np.ascontiguousarray(img8, np.uint8)
+    if img8.size != nx * ny * 3:
+        raise SrrError("write_png needs nx*ny*3 bytes")
+    _check(lib().srr_write_png(path.encode(), nx, ny, _ptr(img8)))
 
 
 def mesh_file_triangles(path: str, flip_uvs: bool = False, flip_winding: bool = False, scale=(1.0, 1.0, 1.0)):
