@@ -16,6 +16,7 @@
 //   sobol  <N> <out.f64>
 //   kat    <name> <n> <seed> <out.bin>             per-function known answers
 //   image  <file> <req_comp> <out.raw>             stbi_load (stb_image v2.19)
+//   builder <name> <nx> <ny> <ns> <maxdepth> <out_prefix>   a reference scene builder
 #define private public
 #define main ref_main
 #include "Raytracing_n.cpp"
@@ -220,15 +221,8 @@ void write(const std::string& path, const void* p, size_t n) {
   fclose(f);
 }
 
-int cmd_render(int argc, char** argv) {
-  if (argc < 8) return 2;
-  RefScene S = build(srr_text::parse(srr_text::read_file(argv[2])));
-  nx = atoi(argv[3]);
-  ny = atoi(argv[4]);
-  ns = atoi(argv[5]);
-  maxDepth = atoi(argv[6]);
-  std::string out = argv[7];
-  counting_world cw(S.world);
+int render_to(hitable* world, hitable* lights, camera* cam, const std::string& out) {
+  counting_world cw(world);
   double** sp = sobol(ns);
   std::vector<float> paths((size_t)nx * ny * ns * 3);
   std::vector<unsigned char> rays((size_t)nx * ny * ns);
@@ -244,10 +238,10 @@ int cmd_render(int argc, char** argv) {
       reseed_path((unsigned)i, (unsigned)j, (unsigned)s);
       float u = float(sp[s][0] + i) / float(nx);
       float v = float(sp[s][1] + j) / float(ny);
-      ray r = S.cam->get_ray(u, v);
+      ray r = cam->get_ray(u, v);
       int depth = 0;
       long long before = cw.n;
-      vec3 c = color(r, &cw, S.lights, &depth);
+      vec3 c = color(r, &cw, lights, &depth);
       size_t p = ((size_t)pix * ns + s);
       paths[p * 3 + 0] = c[0];
       paths[p * 3 + 1] = c[1];
@@ -277,6 +271,41 @@ int cmd_render(int argc, char** argv) {
   printf("{\"paths\": %lld, \"world_rays\": %lld, \"ms\": %.3f, \"msamples_per_s\": %.4f}\n",
          (long long)nx * ny * ns, cw.n, ms, cw.n / (ms * 1e3));
   return 0;
+}
+
+int cmd_render(int argc, char** argv) {
+  if (argc < 8) return 2;
+  RefScene S = build(srr_text::parse(srr_text::read_file(argv[2])));
+  nx = atoi(argv[3]);
+  ny = atoi(argv[4]);
+  ns = atoi(argv[5]);
+  maxDepth = atoi(argv[6]);
+  return render_to(S.world, S.lights, S.cam, argv[7]);
+}
+
+// builder <name> <nx> <ny> <ns> <maxdepth> <out_prefix>: one of the reference's
+// OWN scene builders (Raytracing_n.cpp:108-711), called exactly as main() does
+// (aspect = nx / ny, :895-919) from the state the scene LCG has at main() entry,
+// then rendered like `render`.  The builders open their assets by relative
+// Windows paths ("..\\contents\\..."): the caller runs this in a directory
+// holding entries with those literal names (tests/golden/make_scenes.py).
+int cmd_builder(int argc, char** argv) {
+  if (argc < 8) return 2;
+  std::string name = argv[2];
+  nx = atoi(argv[3]);
+  ny = atoi(argv[4]);
+  ns = atoi(argv[5]);
+  maxDepth = atoi(argv[6]);
+  hitable* world = nullptr;
+  hitable* hl = nullptr;
+  camera* cam = nullptr;
+  float aspect = float(nx) / float(ny);
+  if (name == "random_scene") random_scene(&world, &cam, &hl, aspect);
+  else if (name == "ball_scenes") ball_scenes(&world, &cam, &hl, aspect);
+  else if (name == "ball_orennayar_scenes") ball_orennayar_scenes(&world, &cam, &hl, aspect);
+  else if (name == "final") final(&world, &cam, &hl, aspect);
+  else throw std::runtime_error("builder " + name + " not available (model.h scenes need assimp)");
+  return render_to(world, hl, cam, argv[7]);
 }
 
 // Reference BVH topology in preorder: "N" = interior node, "L a b" = leaf over
@@ -412,6 +441,7 @@ int main(int argc, char** argv) {
     if (c == "sobol") return cmd_sobol(argc, argv);
     if (c == "kat") return cmd_kat(argc, argv);
     if (c == "image") return cmd_image(argc, argv);
+    if (c == "builder") return cmd_builder(argc, argv);
     if (c == "teapot_data") return cmd_teapot_data(argc, argv);
   } catch (const std::exception& e) {
     fprintf(stderr, "ref_harness: %s\n", e.what());

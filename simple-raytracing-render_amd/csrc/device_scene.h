@@ -35,6 +35,7 @@ enum ObjKind : int32_t {
   OBJ_TRI = 3,
   OBJ_MESH = 4,
   OBJ_MEDIUM = 5,
+  OBJ_OBVH = 6,  // bvh_node over analytic hitables (spheres, boxes, rects, ...)
 };
 
 enum XformKind : int32_t { XF_FLIP = 0, XF_TRANSLATE = 1, XF_ROTY = 2, XF_ROTX = 3 };
@@ -74,6 +75,20 @@ struct DMesh {
   int32_t n_nodes, n_tris;
   int32_t node4_off; // root of the 4-wide view in node4[]
   int32_t n_node4;
+};
+
+// bvh_node whose leaves are not bare triangles (e.g. final's 400 boxes and 1,000
+// spheres, Raytracing_n.cpp:483-496, :515-519): the reference-topology BVH2 in the
+// same threaded node format as a mesh, whose leaves name children instead of
+// triangles; each child is a run of DObjs hit with hitable_list semantics (a box
+// is its 6 rects, box.h:31-33), with its transform chain relative to the node.
+struct DObvh {
+  int32_t node_off, n_nodes;
+  int32_t child_off, n_children;
+};
+
+struct DObvhChild {
+  int32_t obj_begin, obj_count;  // into the DObj table
 };
 
 struct DMedium {  // constant_medium.h:4-50

@@ -24,6 +24,8 @@ struct SceneView {  // device pointers into the flattened tables (device_scene.h
   const float4* tri_pos;  // 4 float4 per triangle: p0, p1, p2, pad
   const TriShade* tri_shade;
   const DMedium* media;
+  const DObvh* obvhs;                 // object BVHs (global memory)
+  const DObvhChild* obvh_children;
   const DMat* mats;
   const DTex* texs;
   const uint8_t* images;

@@ -422,27 +422,83 @@ struct ObjHit {
   int prim;  // triangle index for meshes
 };
 
-// hit of one non-medium flattened object (in its local frame)
+// hit of one analytic primitive (sphere, moving sphere, rect, standalone
+// triangle) in its local frame
 template <int TR>
-SRR_D bool basic_hit(const SceneView& S, const DObj& ob, const Ray& lr, float tmin, float tmax, bool is_medium,
-                     ObjHit& h, const TraceCtx& cx) {
+SRR_D bool prim_hit(const SceneView& S, const DObj& ob, const Ray& lr, float tmin, float tmax, bool is_medium,
+                    float& t) {
   switch (ob.kind) {
     case OBJ_SPHERE:
     case OBJ_MSPHERE:
-      return sphere_hit(wload<TR>(S.spheres, ob.idx), ob.kind == OBJ_MSPHERE, lr, tmin, tmax, h.t);
+      return sphere_hit(wload<TR>(S.spheres, ob.idx), ob.kind == OBJ_MSPHERE, lr, tmin, tmax, t);
     case OBJ_RECT: {
       float u, v;
-      return rect_hit(wload<TR>(S.rects, ob.idx), lr, tmin, tmax, h.t, u, v);
+      return rect_hit(wload<TR>(S.rects, ob.idx), lr, tmin, tmax, t, u, v);
     }
     case OBJ_TRI: {
       const DStandaloneTri T = wload<TR>(S.stris, ob.idx);
       V3 p0 = v3(T.p[0], T.p[1], T.p[2]), p1 = v3(T.p[3], T.p[4], T.p[5]), p2 = v3(T.p[6], T.p[7], T.p[8]);
       V3 dir = lr.d / length(lr.d);
       float u, v;
-      bool hh = tri_hit(p0, p1, p2, true, lr.o, dir, h.t, u, v);
-      if (!hh && is_medium) hh = tri_hit(p0, p1, p2, false, lr.o, dir, h.t, u, v);
+      bool hh = tri_hit(p0, p1, p2, true, lr.o, dir, t, u, v);
+      if (!hh && is_medium) hh = tri_hit(p0, p1, p2, false, lr.o, dir, t, u, v);
       return hh;
     }
+  }
+  return false;
+}
+
+// bvh.h:64-93 over an object BVH (device_scene.h DObvh): the threaded walk of
+// mesh_hit -- every node tested against the incoming [tmin, tmax], the
+// reference's visit set, smallest t with ties to the later DFS child (`wins`) --
+// where a leaf child is a run of primitives hit like a hitable_list (its own
+// closest-so-far, from tmax).  Returns the winning primitive's DObj index.
+template <int TR>
+SRR_D bool obvh_hit(const SceneView& S, const DObvh& o, const Ray& r, float tmin, float tmax, bool is_medium,
+                    float& out_t, int& out_obj) {
+  const V3 inv = v3(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+  const int end = o.node_off + o.n_nodes;
+  bool found = false;
+  float best_t = 0;
+  int best_i = -1;
+  for (int node = o.node_off; node < end;) {
+    const float4 lo = S.nodes[2 * node], hi = S.nodes[2 * node + 1];
+    const int skip = __float_as_int(lo.w), leaf = __float_as_int(hi.w);
+    const bool hit = slab(lo, hi, r.o, inv, tmin, tmax);
+    if (hit && leaf >= 0) {
+      const int first = leaf >> 1, count = (leaf & 1) + 1;
+      for (int ci = first; ci < first + count; ++ci) {
+        const DObvhChild c = S.obvh_children[ci];
+        float closest = tmax, ct = 0;
+        int cobj = -1;
+        for (int k = c.obj_begin; k < c.obj_begin + c.obj_count; ++k) {
+          const DObj pb = wload<TR>(S.objs, k);
+          float t;
+          if (prim_hit<TR>(S, pb, chain_in<TR>(S, pb, r), tmin, closest, is_medium, t)) {
+            closest = t;
+            ct = t;
+            cobj = k;
+          }
+        }
+        if (cobj >= 0 && (!found || wins(ct, ci, best_t, best_i))) {
+          found = true;
+          best_t = ct;
+          best_i = ci;
+          out_obj = cobj;
+        }
+      }
+    }
+    node = (hit && leaf < 0) ? node + 1 : skip;
+  }
+  out_t = best_t;
+  return found;
+}
+
+// hit of one non-medium flattened object (in its local frame)
+template <int TR>
+SRR_D bool basic_hit(const SceneView& S, const DObj& ob, const Ray& lr, float tmin, float tmax, bool is_medium,
+                     ObjHit& h, const TraceCtx& cx) {
+  switch (ob.kind) {
     case OBJ_MESH: {
       MeshHit mh;
       const DMesh m = wload<TR>(S.meshes, ob.idx);
@@ -454,8 +510,13 @@ SRR_D bool basic_hit(const SceneView& S, const DObj& ob, const Ray& lr, float tm
       h.prim = mh.tri;
       return true;
     }
+    case OBJ_OBVH:
+      return obvh_hit<TR>(S, S.obvhs[ob.idx], lr, tmin, tmax, is_medium, h.t, h.prim);
+    case OBJ_MEDIUM:
+      return false;
+    default:
+      return prim_hit<TR>(S, ob, lr, tmin, tmax, is_medium, h.t);
   }
-  return false;
 }
 
 // hitable_list::hit (hitable_list.h:21-33) over objects [b, b+n) -- used for a
@@ -551,14 +612,8 @@ SRR_D void sphere_uv(V3 p, float& u, float& v) {  // hitable.h:10-15
   v = (theta + kPi / 2) / kPi;
 }
 
-template <int TR = 0>  // TR & TR_WL: world tables in LDS (plain loads, never cload)
-SRR_D HitRec world_record(const SceneView& S, const Ray& r, const WorldHit& w) {
-  const DObj& ob = S.objs[w.obj];
-  Ray lr = chain_in<TR>(S, ob, r);
-  HitRec h;
-  h.u = 0;  // moving_sphere / constant_medium leave u, v unset in the reference;
-  h.v = 0;  // defined here as 0
-  float t = w.t;
+// record of one primitive (or mesh triangle `prim`) hit at t, in its local frame
+SRR_D void prim_record(const SceneView& S, const DObj& ob, const Ray& lr, float t, int prim, HitRec& h) {
   switch (ob.kind) {
     case OBJ_SPHERE:
     case OBJ_MSPHERE: {
@@ -591,12 +646,12 @@ SRR_D HitRec world_record(const SceneView& S, const Ray& r, const WorldHit& w) {
         p2 = v3(T.p[6], T.p[7], T.p[8]);
         sh = &T.sh;
       } else {
-        const float4* tp = S.tri_pos + kTriStride * (size_t)w.prim;
+        const float4* tp = S.tri_pos + kTriStride * (size_t)prim;
         float4 a = tp[0], b = tp[1], c = tp[2];
         p0 = v3(a.x, a.y, a.z);
         p1 = v3(b.x, b.y, b.z);
         p2 = v3(c.x, c.y, c.z);
-        sh = &S.tri_shade[w.prim];
+        sh = &S.tri_shade[prim];
       }
       V3 dir = lr.d / length(lr.d);
       float tt, u, v;
@@ -621,6 +676,22 @@ SRR_D HitRec world_record(const SceneView& S, const Ray& r, const WorldHit& w) {
       break;
     }
   }
+}
+
+template <int TR = 0>  // TR & TR_WL: world tables in LDS (plain loads, never cload)
+SRR_D HitRec world_record(const SceneView& S, const Ray& r, const WorldHit& w) {
+  const DObj& ob = S.objs[w.obj];
+  Ray lr = chain_in<TR>(S, ob, r);
+  HitRec h;
+  h.u = 0;  // moving_sphere / constant_medium leave u, v unset in the reference;
+  h.v = 0;  // defined here as 0
+  if (ob.kind == OBJ_OBVH) {  // the primitive inside the object BVH, then the node's chain
+    const DObj& in = S.objs[w.prim];
+    prim_record(S, in, chain_in<TR>(S, in, lr), w.t, -1, h);
+    chain_out(S, in, h.p, h.n);
+  } else {
+    prim_record(S, ob, lr, w.t, w.prim, h);
+  }
   chain_out(S, ob, h.p, h.n);
   return h;
 }
@@ -641,7 +712,8 @@ SRR_D int family_of(int mat, int kind, int depth, int max_depth) {
 // Material of a world hit without building its record (the trace kernels bin
 // rays by material family with it).
 SRR_D int hit_material(const SceneView& S, const WorldHit& w) {
-  const DObj ob = S.objs[w.obj];
+  DObj ob = S.objs[w.obj];
+  if (ob.kind == OBJ_OBVH) ob = S.objs[w.prim];
   switch (ob.kind) {
     case OBJ_SPHERE:
     case OBJ_MSPHERE: return S.spheres[ob.idx].mat;

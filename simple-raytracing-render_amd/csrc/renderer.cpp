@@ -44,6 +44,8 @@ int renderer_create(const Scene& sc, int device, srr_renderer** out, std::string
   DObj* objs; DXform* xf; DSphere* sph; DRect* rct; DStandaloneTri* st; DMesh* me; float* nodes; float* n4;
   float* tp; TriShade* ts; DMedium* md; DMat* mt; DTex* tx; uint8_t* im; float* pr; int32_t* pp; DLight* li;
   DCamera* cm;
+  DObvh* ob;
+  DObvhChild* oc;
   std::vector<DCamera> cam{F.cam};
   RCHK(upload(&objs, F.objs, K));
   RCHK(upload(&xf, F.xforms, K));
@@ -56,6 +58,8 @@ int renderer_create(const Scene& sc, int device, srr_renderer** out, std::string
   RCHK(upload(&tp, F.tri_pos, K));
   RCHK(upload(&ts, F.tri_shade, K));
   RCHK(upload(&md, F.media, K));
+  RCHK(upload(&ob, F.obvhs, K));
+  RCHK(upload(&oc, F.obvh_children, K));
   RCHK(upload(&mt, F.mats, K));
   RCHK(upload(&tx, F.texs, K));
   RCHK(upload(&im, F.images, K));
@@ -101,6 +105,8 @@ int renderer_create(const Scene& sc, int device, srr_renderer** out, std::string
   V.tri_pos = (const float4*)tp;
   V.tri_shade = ts;
   V.media = md;
+  V.obvhs = ob;
+  V.obvh_children = oc;
   V.mats = mt;
   V.texs = tx;
   V.images = im;

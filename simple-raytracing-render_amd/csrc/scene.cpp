@@ -556,7 +556,7 @@ struct Flattener {
   Flat& F;
   std::string& err;
   std::map<int, int> mesh_of_bvh;
-  std::vector<DObj> world, bound;
+  std::vector<DObj> world, bound, inner;  // inner: object-BVH children
   std::map<int, int> rect_row, sphere_row;
 
   int chain_push(const std::vector<DXform>& ch) {
@@ -827,6 +827,52 @@ struct Flattener {
     return mesh_of_bvh[h] = (int)F.meshes.size() - 1;
   }
 
+  // bvh_node over other hitables: the same threaded BVH2 records as add_mesh,
+  // leaves naming children (DFS order); each child flattened to DObjs relative to
+  // the node (its own instance chain only).  Children must be analytic
+  // primitives, boxes, lists or instances of those: a mesh or medium nested in
+  // an object BVH is refused.
+  std::map<int, int> obvh_of_bvh;
+  int add_obvh(int h) {
+    auto it = obvh_of_bvh.find(h);
+    if (it != obvh_of_bvh.end()) return it->second;
+    const HBvh& B = S.bvhs[S.obj[h].bvh];
+    DObvh o{};
+    o.node_off = (int)(F.nodes.size() / 8);
+    o.n_nodes = (int)B.nodes.size();
+    o.child_off = (int)F.obvh_children.size();
+    o.n_children = (int)B.leaves.size();
+    for (int l : B.leaves) {
+      std::vector<DObj> tmp;
+      if (!walk(l, {}, tmp, false)) return -1;
+      for (const DObj& d : tmp)
+        if (d.kind != OBJ_SPHERE && d.kind != OBJ_MSPHERE && d.kind != OBJ_RECT && d.kind != OBJ_TRI) {
+          err = "bvh_node over hitables that contain a bvh_node or constant_medium is not supported on the device";
+          return -1;
+        }
+      F.obvh_children.push_back(DObvhChild{(int)inner.size(), (int)tmp.size()});  // rebased in flatten()
+      inner.insert(inner.end(), tmp.begin(), tmp.end());
+    }
+    std::vector<int> size(B.nodes.size(), 1);
+    for (int i = (int)B.nodes.size() - 1; i >= 0; --i)
+      if (B.nodes[i].left >= 0) size[i] = 1 + size[B.nodes[i].left] + size[B.nodes[i].right];
+    for (size_t i = 0; i < B.nodes.size(); ++i) {
+      const HBvh::Node& n = B.nodes[i];
+      int32_t skip = o.node_off + (int32_t)i + size[i];
+      int32_t leaf = -1;
+      if (n.left < 0) {
+        int first = ~n.left, last = ~n.right;
+        leaf = ((first + o.child_off) << 1) | (last != first ? 1 : 0);
+      }
+      float sf, lf;
+      std::memcpy(&sf, &skip, 4);
+      std::memcpy(&lf, &leaf, 4);
+      F.nodes.insert(F.nodes.end(), {n.box.mn[0], n.box.mn[1], n.box.mn[2], sf, n.box.mx[0], n.box.mx[1], n.box.mx[2], lf});
+    }
+    F.obvhs.push_back(o);
+    return obvh_of_bvh[h] = (int)F.obvhs.size() - 1;
+  }
+
   // Appends the objects `h` contributes to `out`, under transform chain `ch`.
   bool walk(int h, std::vector<DXform> ch, std::vector<DObj>& out, bool in_medium) {
     const HObj& o = S.obj[h];
@@ -856,11 +902,13 @@ struct Flattener {
       case H_TRI: emit(OBJ_TRI, add_stri(h)); return true;
       case H_BVH: {
         int m = add_mesh(h);
-        if (m < 0) {
-          err = "bvh_node over non-triangle hitables is not supported on the device yet";
-          return false;
+        if (m >= 0) {
+          emit(OBJ_MESH, m);
+          return true;
         }
-        emit(OBJ_MESH, m);
+        int ob = add_obvh(h);
+        if (ob < 0) return false;
+        emit(OBJ_OBVH, ob);
         return true;
       }
       case H_MEDIUM: {
@@ -940,6 +988,9 @@ int flatten(const Scene& S, Flat& F, std::string& err) {
   F.objs = fl.world;
   for (DObj d : fl.bound) F.objs.push_back(d);
   for (DMedium& m : F.media) m.bnd_begin += F.n_world;
+  const int inner_base = (int)F.objs.size();
+  for (DObj d : fl.inner) F.objs.push_back(d);
+  for (DObvhChild& c : F.obvh_children) c.obj_begin += inner_base;
   for (int k : S.obj[S.lights].kids) {
     if (S.obj[k].kind == H_LIST) {
       err = "nested hitable_list inside the light list is not supported";

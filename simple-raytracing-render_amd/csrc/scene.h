@@ -129,6 +129,8 @@ struct Flat {
   std::vector<float> tri_pos;           // float4 x4 per triangle (p0, p1, p2, pad)
   std::vector<TriShade> tri_shade;
   std::vector<DMedium> media;
+  std::vector<DObvh> obvhs;
+  std::vector<DObvhChild> obvh_children;
   std::vector<DMat> mats;
   std::vector<DTex> texs;
   std::vector<uint8_t> images;

@@ -12,7 +12,10 @@ oracles consume, so one scene definition drives every consumer.
 """
 from __future__ import annotations
 
+import hashlib
+import os
 import struct
+import tempfile
 from dataclasses import dataclass
 
 # State of the reference's global 48-bit LCG after perlin.h's static
@@ -94,6 +97,31 @@ class Scene:
         k = {"sky": 0, "wood": 1, "checker": 2}[kind]
         t = Tex(self._id("tex"))
         self._emit("tex", t.id, "image_gen", w, h, seed, k)
+        return t
+
+    def image_texture_file(self, path: str) -> Tex:
+        """``image_texture(stbi_load(path, &tx, &ty, &tn, 0), tx, ty)`` -- the
+        builders' idiom (Raytracing_n.cpp:269-270, :614-616, :631-632).  The file
+        is decoded now by srr's stb-exact decoder (srr_image_load) and recorded as
+        an ``image_raw`` texture: the 3 bytes per texel image_texture addresses
+        (texture.h:58-70), cached under $SRR_IMAGE_CACHE (default
+        <tmp>/srr_images) by content hash."""
+        from .capi import image_load  # the decoder lives in libsrr
+        px, _ = image_load(path, 0)
+        h, w, ch = px.shape
+        if ch < 3:
+            raise ValueError(f"{path}: image_texture needs 3 or 4 channels, file has {ch}")
+        raw = px.reshape(-1)[: w * h * 3].tobytes()
+        cache = os.environ.get("SRR_IMAGE_CACHE") or os.path.join(tempfile.gettempdir(), "srr_images")
+        os.makedirs(cache, exist_ok=True)
+        fn = os.path.join(cache, f"{hashlib.sha256(raw).hexdigest()[:24]}_{w}x{h}.rgb")
+        if not (os.path.exists(fn) and os.path.getsize(fn) == len(raw)):
+            tmp = f"{fn}.{os.getpid()}.tmp"
+            with open(tmp, "wb") as f:
+                f.write(raw)
+            os.replace(tmp, fn)
+        t = Tex(self._id("tex"))
+        self._emit("tex", t.id, "image_raw", w, h, fn)
         return t
 
     def checker_texture(self, t0: Tex, t1: Tex) -> Tex:
