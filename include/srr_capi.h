@@ -199,6 +199,13 @@ int srr_write_png(const char* path, int nx, int ny, const unsigned char* rgb8);
 int srr_image_load(const char* path, int req_comp, int* x, int* y, int* comp, unsigned char** out);
 void srr_image_free(unsigned char* pixels);
 
+/* Test infrastructure: run the device (HIP) implementation of one reference
+ * function on KAT records laid out as oracle/ref/kat.inc writes them (inputs
+ * first, outputs overwritten in place): "erf", "beckmann11", "beckmann_dist",
+ * "beckmann_pdf", "cosine_pdf", "orennayar_pdf", "dielectric", "metal",
+ * "triangle", "aabb"; and "sqrt" (records x, sqrtf(x)).  Needs a GPU. */
+int srr_device_kat(const char* name, int n, int width, float* records);
+
 /* Sobol (0,2)-points of Raytracing_n.cpp:721-812, out[n][2]. */
 int srr_sobol_points(int n, double* out);
 

@@ -448,6 +448,64 @@ int srr_image_load(const char* path, int req_comp, int* x, int* y, int* comp, un
 
 void srr_image_free(unsigned char* pixels) { free(pixels); }
 
+int srr_device_kat(const char* name, int n, int width, float* records) {
+  if (!name || !records || n <= 0 || width <= 0) return fail(SRR_EINVAL, "bad KAT arguments");
+  static const char* kNames[] = {"erf", "beckmann11", "beckmann_dist", "beckmann_pdf", "cosine_pdf",
+                                 "orennayar_pdf", "dielectric", "metal", "triangle", "aabb", "sqrt"};
+  static const int kWidth[] = {3, 5, 16, 21, 21, 21, 14, 14, 26, 15, 2};
+  int kind = -1;
+  for (int k = 0; k < 11; ++k)
+    if (!strcmp(name, kNames[k])) kind = k;
+  if (kind < 0) return fail(SRR_EINVAL, std::string("no device KAT named ") + name);
+  if (width != kWidth[kind]) return fail(SRR_EINVAL, std::string("KAT ") + name + ": unexpected record width");
+  // host-side parameters the scene builder would compute (material ctors, face normals)
+  std::vector<float> aux(4 * (size_t)n, 0.f);
+  std::vector<DStandaloneTri> tris(kind == 8 ? n : 1);
+  Scene hs;
+  for (int q = 0; q < n; ++q) {
+    const float* r = records + (size_t)q * width;
+    if (kind == 2 || kind == 3) {
+      const float prm[4] = {r[0], r[1], 0, 0};
+      const HMat& m = hs.mat[hs.material(MAT_BECKMANN, -1, prm)];
+      aux[4 * q] = m.p[0];
+      aux[4 * q + 1] = m.p[1];
+    } else if (kind == 4 || kind == 5) {
+      const float prm[4] = {r[0], 0, 0, 0};
+      const HMat& m = hs.mat[hs.material(MAT_ORENNAYAR, -1, prm)];
+      aux[4 * q] = m.p[0];
+      aux[4 * q + 1] = m.p[1];
+    } else if (kind == 8) {  // triangle(p0, p1, p2, mat, uv0, uv1, uv2) with face normals (kat.inc)
+      const float uv9[9] = {0.1f, 0.2f, 0, 0.7f, 0.1f, 0, 0.3f, 0.9f, 0};
+      const int h = hs.triangle(r, -1, uv9, nullptr);
+      const HTri& t = hs.tris[hs.obj[h].tri];
+      DStandaloneTri& d = tris[q];
+      std::memcpy(d.p, t.p, 36);
+      std::memcpy(d.sh.n, t.n, 36);
+      for (int k = 0; k < 3; ++k) d.sh.uv[2 * k] = t.uv[3 * k], d.sh.uv[2 * k + 1] = t.uv[3 * k + 1];
+      d.sh.mat = -1;
+    }
+  }
+  float* d_rec = nullptr;
+  float* d_aux = nullptr;
+  DStandaloneTri* d_tris = nullptr;
+  const size_t rb = (size_t)n * width * sizeof(float);
+  int rc = 0;
+  if (hipMalloc((void**)&d_rec, rb) != hipSuccess || hipMalloc((void**)&d_aux, aux.size() * 4) != hipSuccess ||
+      hipMalloc((void**)&d_tris, tris.size() * sizeof(DStandaloneTri)) != hipSuccess)
+    rc = fail(SRR_ENOMEM, "device allocation failed");
+  if (!rc && (hipMemcpy(d_rec, records, rb, hipMemcpyHostToDevice) != hipSuccess ||
+              hipMemcpy(d_aux, aux.data(), aux.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+              hipMemcpy(d_tris, tris.data(), tris.size() * sizeof(DStandaloneTri), hipMemcpyHostToDevice) != hipSuccess))
+    rc = fail(SRR_EIO, "copy to device failed");
+  if (!rc && launch_kat(kind, n, width, d_rec, d_aux, d_tris) < 0) rc = fail(SRR_EIO, "KAT kernel launch failed");
+  if (!rc && (hipDeviceSynchronize() != hipSuccess || hipMemcpy(records, d_rec, rb, hipMemcpyDeviceToHost) != hipSuccess))
+    rc = fail(SRR_EIO, "KAT kernel failed");
+  (void)hipFree(d_rec);
+  (void)hipFree(d_aux);
+  (void)hipFree(d_tris);
+  return rc;
+}
+
 int srr_teapot_vertices(float scale, int divs, float* out) {
   if (divs < 1 || divs > 400) return fail(SRR_EINVAL, "teapot divs out of range");
   std::vector<float> p;

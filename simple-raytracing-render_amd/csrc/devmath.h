@@ -4,9 +4,10 @@
 // track it on gfx950:
 //  * kernels are compiled with -ffp-contract=off (no FMA contraction), and HIP's
 //    default correctly rounded f32 division / sqrt;
-//  * a float libm call of the reference (sinf, cosf, expf, logf, powf, acosf,
-//    asinf, atan2f) is evaluated here in double and rounded once to float:
-//    glibc's float routines are (nearly always) correctly rounded, and so is this;
+//  * the reference's float libm calls run glibc's own algorithms and tables
+//    (glibc_mathf.h: sinf, cosf, expf, logf, powf, acosf -- bit-exact with the
+//    host's libm); asinf and atan2f (sphere uv only) are evaluated in double and
+//    rounded once, which matches glibc except in the last bit of rare inputs;
 //  * double libm calls (sin/cos/log/pow of double) use the device double libm.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -18,15 +19,50 @@ namespace dev {
 
 #define SRR_D __device__ __forceinline__
 
+// Correctly rounded f32 sqrt.  v_sqrt_f32 (what __fsqrt_rn / sqrtf lower to on
+// gfx950) is accurate to 1 ulp, not correctly rounded; the reference's sqrtf is.
+// One step picks among s - 1ulp, s, s + 1ulp by the sign of the exact residual
+// x - s'*s (fma), with the usual 2^32 pre-scaling of tiny inputs.
+SRR_D float rsqrt_exact(float x) {
+  const bool tiny = x < 0x1p-96f;
+  const float sx = tiny ? x * 0x1p+32f : x;
+  float s = __builtin_amdgcn_sqrtf(sx);
+  if (sx > 0.0f && sx < INFINITY) {
+    const float dn = __int_as_float(__float_as_int(s) - 1);
+    const float up = __int_as_float(__float_as_int(s) + 1);
+    const float vp = __builtin_fmaf(-dn, s, sx);
+    const float vs = __builtin_fmaf(-up, s, sx);
+    s = vp <= 0.0f ? dn : s;
+    s = vs > 0.0f ? up : s;
+  }
+  return tiny ? s * 0x1p-16f : s;
+}
+
+}  // namespace dev
+}  // namespace srr
+
+#include "glibc_mathf.h"
+
+namespace srr {
+namespace dev {
+
+#ifndef SRR_LIBM_DOUBLE  // (A/B builds only: -DSRR_LIBM_DOUBLE rounds double libm results instead)
+SRR_D float rsin(float x) { return gm::sinf_(x); }
+SRR_D float rcos(float x) { return gm::cosf_(x); }
+SRR_D float rexp(float x) { return gm::expf_(x); }
+SRR_D float rlog(float x) { return gm::logf_(x); }
+SRR_D float rpow(float x, float y) { return gm::powf_(x, y); }
+SRR_D float racos(float x) { return gm::acosf_(x); }
+#else
 SRR_D float rsin(float x) { return (float)::sin((double)x); }
 SRR_D float rcos(float x) { return (float)::cos((double)x); }
 SRR_D float rexp(float x) { return (float)::exp((double)x); }
 SRR_D float rlog(float x) { return (float)::log((double)x); }
 SRR_D float rpow(float x, float y) { return (float)::pow((double)x, (double)y); }
 SRR_D float racos(float x) { return (float)::acos((double)x); }
+#endif
 SRR_D float rasin(float x) { return (float)::asin((double)x); }
 SRR_D float ratan2(float y, float x) { return (float)::atan2((double)y, (double)x); }
-SRR_D float rsqrt_exact(float x) { return __fsqrt_rn(x); }  // correctly rounded
 SRR_D float rdiv(float a, float b) { return __fdiv_rn(a, b); }
 
 static constexpr double kPi = 3.14159265358979323846;  // mathf.h:10

@@ -1,0 +1,293 @@
+// The reference's float libm calls, rounded exactly as on its host.
+//
+// The reference calls expf, logf, powf, sinf, cosf and acosf (via <cmath>'s float
+// overloads: Erf / ErfInv common.h:26-78, the Beckmann sampler and D()
+// microfacet_distribution.h:34-107,155-172, random_cosine_direction pdf.h:10-18,
+// sphere light sampling sphere.h:7-15, Perlin noise).  glibc >= 2.28 computes
+// them with table-driven double-precision algorithms (from ARM's
+// optimized-routines) that are accurate but not always correctly rounded: a
+// correctly rounded device libm differs in the last bit a few times per
+// thousand calls, and a Beckmann path can turn such a bit into a different
+// scattering direction.  These are the same algorithms on the same tables
+// (glibc_mathf_tables.inc, extracted from libm.so.6 by tools/gen_glibc_mathf.py)
+// with the fused multiply-adds of glibc's x86-64 FMA variants (selected on any
+// CPU with FMA, e.g. e_expf-fma.c), so the device returns the host's float bit
+// for bit.  tools/check_glibc_mathf.cpp compares them with libm over every float
+// input (expf, logf, sinf, cosf, acosf) and over sampled (x, y) pairs (powf):
+// all bit-exact except expf at 2 of the 2^32 inputs (1 ulp, |x| > 32).  acosf
+// is glibc's fdlibm float routine, restated.
+//
+// Special powf operands (zero / inf / nan / negative or subnormal x, results
+// beyond 2^+-126) take the double-precision route; the reference never meets them.
+#pragma once
+#include <cstdint>
+#include <cstring>
+
+#if defined(__HIPCC__)
+#define GM_FN __device__ __forceinline__
+#define GM_TAB __device__ __constant__ const
+#define GM_FMA(a, b, c) __builtin_fma((a), (b), (c))
+#define GM_SQRTF(x) ::srr::dev::rsqrt_exact(x)  // correctly rounded (devmath.h)
+#else
+#include <cmath>
+#define GM_FN static inline
+#define GM_TAB static const
+#define GM_FMA(a, b, c) std::fma((a), (b), (c))
+#define GM_SQRTF(x) std::sqrt((float)(x))
+#endif
+
+namespace srr {
+namespace gm {
+
+#include "glibc_mathf_tables.inc"
+
+GM_FN uint32_t asuint(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  return u;
+}
+GM_FN float asfloat(uint32_t u) {
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+GM_FN uint64_t asuint64(double f) {
+  uint64_t u;
+  std::memcpy(&u, &f, 8);
+  return u;
+}
+GM_FN double asdouble(uint64_t u) {
+  double f;
+  std::memcpy(&f, &u, 8);
+  return f;
+}
+GM_FN uint32_t top12(float x) { return asuint(x) >> 20; }
+
+// e_expf.c: exp(x) = 2^(k/32) * 2^(r/32), k = round(x * 32/ln2)
+GM_FN float expf_(float x) {
+  const uint32_t abstop = top12(x) & 0x7ff;
+  if (abstop >= top12(88.0f)) {
+    if (asuint(x) == asuint(-INFINITY)) return 0.0f;
+    if (abstop >= top12(INFINITY)) return x + x;
+    if (x > 0x1.62e42ep6f) return INFINITY;
+    if (x < -0x1.9fe368p6f) return 0.0f;
+  }
+  const double xd = (double)x;
+  const double z = kExpfInvLn2N * xd;
+  double kd = z + kExp2fShift;
+  const uint64_t ki = asuint64(kd);
+  kd -= kExp2fShift;
+  const double r = z - kd;
+  uint64_t t = kExp2fTab[ki % 32];
+  t += ki << (52 - 5);
+  const double s = asdouble(t);
+  const double zz = GM_FMA(kExp2fPolyScaled[0], r, kExp2fPolyScaled[1]);
+  const double r2 = r * r;
+  double y = GM_FMA(kExp2fPolyScaled[2], r, 1.0);
+  y = GM_FMA(zz, r2, y);
+  y = y * s;
+  return (float)y;
+}
+
+// e_logf.c: log(x) = log1p(z/c - 1) + log(c) + k ln2
+GM_FN float logf_(float x) {
+  uint32_t ix = asuint(x);
+  if (ix == 0x3f800000) return 0.0f;
+  if (ix - 0x00800000 >= 0x7f800000 - 0x00800000) {
+    if (ix * 2 == 0) return -INFINITY;
+    if (ix == 0x7f800000) return x;
+    if ((ix & 0x80000000) || ix * 2 >= 0xff000000) return (x - x) / (x - x);
+    ix = asuint(x * 0x1p23f);  // subnormal: normalise
+    ix -= 23 << 23;
+  }
+  const uint32_t tmp = ix - 0x3f330000;
+  const int i = (tmp >> (23 - 4)) % 16;
+  const int k = (int32_t)tmp >> 23;
+  const uint32_t iz = ix - (tmp & 0xff800000u);
+  const double invc = kLogfTab[2 * i], logc = kLogfTab[2 * i + 1];
+  const double z = (double)asfloat(iz);
+  const double r = GM_FMA(z, invc, -1.0);
+  const double y0 = GM_FMA((double)k, kLogfLn2, logc);
+  const double r2 = r * r;
+  double y = GM_FMA(kLogfPoly[1], r, kLogfPoly[2]);
+  y = GM_FMA(kLogfPoly[0], r2, y);
+  y = GM_FMA(y, r2, y0 + r);
+  return (float)y;
+}
+
+// e_powf.c: exp2(y * log2(x)), both in double, x > 0 normal and y finite non-zero
+GM_FN float powf_(float x, float y) {
+  const uint32_t ix = asuint(x), iy = asuint(y);
+  const bool y_zeroinfnan = 2 * iy - 1 >= 2u * 0x7f800000 - 1;
+  if (ix - 0x00800000 >= 0x7f800000 - 0x00800000 || y_zeroinfnan)
+    return (float)pow((double)x, (double)y);  // special operands, negative / subnormal x
+  // log2_inline
+  const uint32_t tmp = ix - 0x3f330000;
+  const int i = (tmp >> (23 - 4)) % 16;
+  const uint32_t top = tmp & 0xff800000u;
+  const uint32_t iz = ix - top;
+  const int k = (int32_t)top >> 23;
+  const double invc = kPowfLog2Tab[2 * i], logc = kPowfLog2Tab[2 * i + 1];
+  const double z = (double)asfloat(iz);
+  const double r = GM_FMA(z, invc, -1.0);
+  const double y0 = logc + (double)k;
+  const double r2 = r * r;
+  double yy = GM_FMA(kPowfLog2Poly[0], r, kPowfLog2Poly[1]);
+  const double p = GM_FMA(kPowfLog2Poly[2], r, kPowfLog2Poly[3]);
+  const double r4 = r2 * r2;
+  double q = GM_FMA(kPowfLog2Poly[4], r, y0);
+  q = GM_FMA(p, r2, q);
+  const double logx = GM_FMA(yy, r4, q);
+  const double ylogx = (double)y * logx;
+  if ((asuint64(ylogx) >> 47 & 0xffff) >= asuint64(126.0) >> 47)
+    return (float)pow((double)x, (double)y);  // |y log2 x| >= 126: over/underflow range
+  // exp2_inline (sign_bias 0)
+  double kd = ylogx + kExp2fShiftScaled;
+  const uint64_t ki = asuint64(kd);
+  kd -= kExp2fShiftScaled;
+  const double rr = ylogx - kd;
+  uint64_t t = kExp2fTab[ki % 32];
+  t += ki << (52 - 5);
+  const double s = asdouble(t);
+  const double zz = GM_FMA(kExp2fPoly[0], rr, kExp2fPoly[1]);
+  const double rr2 = rr * rr;
+  double e = GM_FMA(kExp2fPoly[2], rr, 1.0);
+  e = GM_FMA(zz, rr2, e);
+  return (float)(e * s);
+}
+
+// sincosf.h: polynomial of quadrant n on the reduced argument
+GM_FN float sinf_poly(double x, double x2, int t, int n) {
+  const double* p = kSincosf[t];
+  if ((n & 1) == 0) {  // p: sign[4], hpi_inv, hpi, c0, c1, s1, c2, s2, c3, s3, c4
+    const double x3 = x * x2;
+    const double s1 = GM_FMA(x2, p[12], p[10]);
+    const double x7 = x3 * x2;
+    const double s = GM_FMA(x3, p[8], x);
+    return (float)GM_FMA(x7, s1, s);
+  }
+  const double x4 = x2 * x2;
+  const double c2 = GM_FMA(x2, p[13], p[11]);
+  const double c1 = GM_FMA(x2, p[7], p[6]);
+  const double x6 = x4 * x2;
+  const double c = GM_FMA(x4, p[9], c1);
+  return (float)GM_FMA(x6, c2, c);
+}
+
+// reduce_fast: n = round(x * 2/pi) (from x * 2^24 * 2/pi), x - n pi/2
+GM_FN double reduce_fast(double x, int& n) {
+  const double r = x * kSincosf[0][4];
+  n = ((int32_t)r + 0x800000) >> 24;
+  return GM_FMA(-(double)n, kSincosf[0][5], x);
+}
+
+// reduce_large: |y| >= 120, Payne-Hanek with 4/pi to 192 bits; x in
+// [-pi/4, pi/4] scaled by 2^62 in an integer, quadrant n
+GM_FN double reduce_large(uint32_t xi, int& n) {
+  const uint32_t* arr = &kInvPio4[(xi >> 26) & 15];
+  const int shift = (xi >> 23) & 7;
+  xi = (xi & 0xffffff) | 0x800000;
+  xi <<= shift;
+  uint64_t res0 = (uint32_t)(xi * arr[0]);
+  const uint64_t res1 = (uint64_t)xi * arr[4];
+  const uint64_t res2 = (uint64_t)xi * arr[8];
+  res0 = (res2 >> 32) | (res0 << 32);
+  res0 += res1;
+  const uint64_t nn = (res0 + (1ULL << 61)) >> 62;
+  res0 -= nn << 62;
+  n = (int)nn;
+  return (double)(int64_t)res0 * 0x1.921fb54442d18p-62;
+}
+
+GM_FN float sinf_(float y) {
+  const uint32_t a = top12(y) & 0x7ff;
+  double x = y;
+  if (a < (top12(0x1.921fb6p-1f) & 0x7ff)) {  // |y| < pi/4
+    if (a < (top12(0x1p-12f) & 0x7ff)) return y;
+    return sinf_poly(x, x * x, 0, 0);
+  }
+  if (a < (top12(120.0f) & 0x7ff)) {
+    int n;
+    x = reduce_fast(x, n);
+    const double s = kSincosf[0][n & 3];
+    const int t = (n & 2) ? 1 : 0;
+    return sinf_poly(x * s, x * x, t, n);
+  }
+  if (a < (top12(INFINITY) & 0x7ff)) {
+    const uint32_t xi = asuint(y);
+    const int sign = xi >> 31;
+    int n;
+    x = reduce_large(xi, n);
+    const double s = kSincosf[0][(n + sign) & 3];
+    const int t = ((n + sign) & 2) ? 1 : 0;
+    return sinf_poly(x * s, x * x, t, n);
+  }
+  return y - y;  // inf / nan
+}
+
+GM_FN float cosf_(float y) {
+  const uint32_t a = top12(y) & 0x7ff;
+  double x = y;
+  if (a < (top12(0x1.921fb6p-1f) & 0x7ff)) {
+    if (a < (top12(0x1p-12f) & 0x7ff)) return 1.0f;
+    return sinf_poly(x, x * x, 0, 1);
+  }
+  if (a < (top12(120.0f) & 0x7ff)) {
+    int n;
+    x = reduce_fast(x, n);
+    const double s = kSincosf[0][n & 3];
+    const int t = (n & 2) ? 1 : 0;
+    return sinf_poly(x * s, x * x, t, n ^ 1);
+  }
+  if (a < (top12(INFINITY) & 0x7ff)) {
+    const uint32_t xi = asuint(y);
+    const int sign = xi >> 31;
+    int n;
+    x = reduce_large(xi, n);
+    const double s = kSincosf[0][(n + sign) & 3];
+    const int t = ((n + sign) & 2) ? 1 : 0;
+    return sinf_poly(x * s, x * x, t, n ^ 1);
+  }
+  return y - y;  // inf / nan
+}
+
+// e_acosf.c (fdlibm's float acos, which glibc 2.35 keeps): float arithmetic,
+// rational approximation on z = x^2 or z = (1 -+ x)/2
+GM_FN float acosf_(float x) {
+  const float one = 1.0f, pi = 3.1415925026e+00f, pio2_hi = 1.5707962513e+00f, pio2_lo = 7.5497894159e-08f;
+  const float pS0 = 1.6666667163e-01f, pS1 = -3.2556581497e-01f, pS2 = 2.0121252537e-01f,
+              pS3 = -4.0055535734e-02f, pS4 = 7.9153501429e-04f, pS5 = 3.4793309169e-05f;
+  const float qS1 = -2.4033949375e+00f, qS2 = 2.0209457874e+00f, qS3 = -6.8828397989e-01f, qS4 = 7.7038154006e-02f;
+  const int32_t hx = (int32_t)asuint(x), ix = hx & 0x7fffffff;
+  if (ix == 0x3f800000) return hx > 0 ? 0.0f : pi + 2.0f * pio2_lo;
+  if (ix > 0x3f800000) return (x - x) / (x - x);
+  if (ix < 0x3f000000) {  // |x| < 0.5
+    if (ix <= 0x32800000) return pio2_hi + pio2_lo;
+    const float z = x * x;
+    const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+    const float q = one + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+    const float r = p / q;
+    return pio2_hi - (x - (pio2_lo - x * r));
+  }
+  if (hx < 0) {  // x < -0.5
+    const float z = (one + x) * 0.5f;
+    const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+    const float q = one + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+    const float s = GM_SQRTF(z);
+    const float r = p / q;
+    const float w = r * s - pio2_lo;
+    return pi - 2.0f * (s + w);
+  }
+  const float z = (one - x) * 0.5f;  // x > 0.5
+  const float s = GM_SQRTF(z);
+  const float df = asfloat(asuint(s) & 0xfffff000u);
+  const float c = (z - df * df) / (s + df);
+  const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+  const float q = one + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+  const float r = p / q;
+  const float w = r * s + c;
+  return 2.0f * (df + w);
+}
+
+}  // namespace gm
+}  // namespace srr

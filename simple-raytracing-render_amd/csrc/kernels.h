@@ -103,6 +103,8 @@ constexpr int kPathsLdsNodes = 96;         // BVH4 nodes cached in LDS by k_path
 void dump_trace_timing();
 int paths_lanes_per_device(const SceneView& S, int device);  // persistent grid capacity
 void launch_paths(const SceneView& S, const PathWork& W, int all_families, hipStream_t st);
+// device known-answer tests (srr_device_kat); kind = dev::KatKind
+int launch_kat(int kind, int n, int w, float* d_rec, const float* d_aux, const DStandaloneTri* d_tris);
 void launch_accumulate_window(const float* sample, int npix, int spp_w, float* acc, hipStream_t st);
 void launch_raygen(const SceneView& S, const PathState& P, const BatchInfo& B, hipStream_t st);
 void launch_trace(const SceneView& S, const PathState& P, const int* active, const int* count, int max_n,

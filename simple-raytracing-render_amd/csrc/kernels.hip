@@ -947,10 +947,8 @@ SRR_D V3 random_cosine_direction(Rng& rng) {
   float r2 = drand(rng);
   float phi = 2 * kPi * r1;
   float z = rsqrt_exact(1 - r2);
-  double sp, cp;  // cos / sin of the same float (evaluated in double, rounded once: rcos / rsin)
-  ::sincos((double)phi, &sp, &cp);
-  float x = (float)cp * 2 * rsqrt_exact(r2);
-  float y = (float)sp * 2 * rsqrt_exact(r2);
+  float x = rcos(phi) * 2 * rsqrt_exact(r2);  // cosf / sinf (glibc_mathf.h)
+  float y = rsin(phi) * 2 * rsqrt_exact(r2);
   return v3(x, y, z);
 }
 
@@ -1981,6 +1979,141 @@ __global__ void k_finish(const float* acc, float* mean, int64_t n, int ns) {
   mean[i] = acc[i] * k;
 }
 
+// ------------------------------------------------- device known-answer tests
+// Test infrastructure (srr_device_kat): the product's device functions on the
+// reference's KAT records (tests/golden/kat_*.bin, layouts in oracle/ref/kat.inc):
+// inputs are read from each record and the outputs written back in place, so a
+// test can compare them bit for bit with the reference's outputs.
+// aux: 4 host-computed floats per record (Beckmann alphas, Oren-Nayar A / B).
+enum KatKind : int { KAT_ERF, KAT_BECK11, KAT_BECK_DIST, KAT_BECK_PDF, KAT_COSINE, KAT_ORENNAYAR, KAT_DIELECTRIC,
+                     KAT_METAL, KAT_TRIANGLE, KAT_AABB, KAT_SQRT };
+
+SRR_D V3 kat3(const float* p) { return v3(p[0], p[1], p[2]); }
+SRR_D void kat_put3(float* p, V3 v) { p[0] = v.x, p[1] = v.y, p[2] = v.z; }
+SRR_D uint64_t kat_lcg(const float* p) { return (uint64_t)p[0] | ((uint64_t)p[1] << 24); }
+SRR_D void kat_put_lcg(float* p, uint64_t s) { p[0] = (float)(s & 0xFFFFFF), p[1] = (float)((s >> 24) & 0xFFFFFF); }
+SRR_D uint64_t kat_pcg(const float* p) {
+  uint64_t s = 0;
+  for (int k = 0; k < 4; ++k) s |= (uint64_t)p[k] << (16 * k);
+  return s;
+}
+SRR_D void kat_put_pcg(float* p, uint64_t s) {
+  for (int k = 0; k < 4; ++k) p[k] = (float)((s >> (16 * k)) & 0xFFFF);
+}
+
+__global__ void k_kat(int kind, int n, int w, float* rec, const float* aux, const DStandaloneTri* tris) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= n) return;
+  float* r = rec + (size_t)q * w;
+  const float* a = aux + 4 * (size_t)q;
+  switch (kind) {
+    case KAT_ERF:
+      r[1] = Erf(r[0]);
+      r[2] = ErfInv(r[0]);
+      break;
+    case KAT_BECK11:
+      beckmann_sample11(r[0], r[1], r[2], r[3], r[4]);
+      break;
+    case KAT_BECK_DIST: {
+      const Beck d{a[0], a[1]};
+      const V3 wo = kat3(r + 2);
+      const V3 wh = beckmann_sample_wh(d, wo, r[5], r[6]);
+      r[7] = d.ax;
+      r[8] = d.ay;
+      kat_put3(r + 9, wh);
+      r[12] = d.D(wh);
+      r[13] = d.G(wo, wh);
+      r[14] = d.Pdf(wo, wh);
+      r[15] = d.Lambda(wo);
+      break;
+    }
+    case KAT_BECK_PDF: {
+      Bsdf f;
+      f.kind = MAT_BECKMANN;
+      f.n = kat3(r + 2);
+      f.uvw = onb_from_w(f.n);
+      f.dist = Beck{a[0], a[1]};
+      f.beck_pdf = 0;
+      const V3 wo = kat3(r + 5);
+      Rng rng{0, kat_pcg(r + 8)};
+      const V3 wi = bsdf_generate<true>(f, wo, rng);
+      kat_put3(r + 12, wi);
+      r[15] = bsdf_value<true>(f, wo, wi);
+      r[16] = scattering_pdf<true>(f, f.n, wo, wi);
+      kat_put_pcg(r + 17, rng.pcg);
+      break;
+    }
+    case KAT_COSINE:
+    case KAT_ORENNAYAR: {
+      Bsdf f;
+      f.kind = kind == KAT_COSINE ? MAT_LAMBERTIAN : MAT_ORENNAYAR;
+      f.n = kat3(r + 1);
+      f.uvw = onb_from_w(f.n);
+      f.A = a[0];
+      f.B = a[1];
+      const V3 wo = kat3(r + 4);
+      Rng rng{kat_lcg(r + 7), 0};
+      const V3 d = bsdf_generate<false>(f, wo, rng);
+      r[9] = a[0];
+      r[10] = a[1];
+      kat_put3(r + 11, d);
+      r[14] = bsdf_value<false>(f, wo, d);
+      r[15] = bsdf_value<false>(f, wo, kat3(r + 16));
+      kat_put_lcg(r + 19, rng.lcg);
+      break;
+    }
+    case KAT_DIELECTRIC:
+    case KAT_METAL: {
+      DMat M{};
+      if (kind == KAT_DIELECTRIC) {
+        M.kind = MAT_DIELECTRIC;
+        M.p[0] = r[0];
+      } else {
+        M.kind = MAT_METAL;
+        M.p[0] = M.p[1] = M.p[2] = 0.5f;
+        M.p[3] = r[0] < 1 ? r[0] : 1;
+      }
+      Rng rng{kat_lcg(r + 7), 0};
+      float4 rc;
+      bool sp;
+      V3 nd;
+      float nt;
+      scatter<FAM_SPEC>(SceneView{}, M, kat3(r + 1), 0.25f, v3(1, 2, 3), kat3(r + 4), 0, 0, rng, rc, sp, nd, nt);
+      kat_put3(r + 9, nd);
+      kat_put_lcg(r + 12, rng.lcg);
+      break;
+    }
+    case KAT_TRIANGLE: {
+      SceneView S{};
+      S.stris = tris;
+      const DObj ob{OBJ_TRI, 0, 0, q};
+      const Ray ray{kat3(r + 9), kat3(r + 12), 0.0f};
+      float t = 0;
+      const bool h = prim_hit<TR_WL>(S, ob, ray, 0.001f, FLT_MAX, r[15] != 0, t);
+      HitRec hr;
+      hr.u = hr.v = 0;
+      hr.p = hr.n = v3(0.f);
+      if (h) prim_record(S, ob, ray, t, -1, hr);
+      r[16] = h ? 1.f : 0.f;
+      r[17] = h ? t : 0;
+      r[18] = hr.u;
+      r[19] = hr.v;
+      kat_put3(r + 20, hr.n);
+      kat_put3(r + 23, hr.p);
+      break;
+    }
+    case KAT_SQRT:
+      r[1] = rsqrt_exact(r[0]);
+      break;
+    case KAT_AABB: {
+      const V3 d = kat3(r + 9);
+      r[14] = slab(make_float4(r[0], r[1], r[2], 0), make_float4(r[3], r[4], r[5], 0), kat3(r + 6),
+                   v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z), r[12], r[13]) ? 1.f : 0.f;
+      break;
+    }
+  }
+}
+
 }  // namespace dev
 
 // ------------------------------------------------------------ launch shims
@@ -2176,6 +2309,11 @@ void launch_paths(const SceneView& S, const PathWork& W, int all_families, hipSt
   }
 #undef SRR_LAUNCH_PATHS_B
 #undef SRR_LAUNCH_PATHS
+}
+
+int launch_kat(int kind, int n, int w, float* d_rec, const float* d_aux, const DStandaloneTri* d_tris) {
+  hipLaunchKernelGGL(dev::k_kat, dim3((n + 63) / 64), dim3(64), 0, 0, kind, n, w, d_rec, d_aux, d_tris);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
 void launch_accumulate_window(const float* sample, int npix, int spp_w, float* acc, hipStream_t st) {

@@ -10,7 +10,7 @@ import os
 import numpy as np
 
 PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG, "libsrr.so")
+LIB_PATH = os.environ.get("SRR_LIB") or os.path.join(PKG, "libsrr.so")  # SRR_LIB: A/B builds
 _LIB = None
 
 FLAG_SORT_MATERIALS = 1
