@@ -156,29 +156,34 @@ GM_FN float powf_(float x, float y) {
   return (float)(e * s);
 }
 
-// sincosf.h: polynomial of quadrant n on the reduced argument
-GM_FN float sinf_poly(double x, double x2, int t, int n) {
-  const double* p = kSincosf[t];
-  if ((n & 1) == 0) {  // p: sign[4], hpi_inv, hpi, c0, c1, s1, c2, s2, c3, s3, c4
+// sincosf.h: polynomial of quadrant n on the reduced argument.  glibc picks
+// __sincosf_table[1] for quadrants with n & 2, which is table 0 with the cosine
+// coefficients negated, so that case is the cosine polynomial negated (exact).
+GM_FN float sinf_poly(double x, double x2, bool neg_cos, int n) {
+  if ((n & 1) == 0) {
     const double x3 = x * x2;
-    const double s1 = GM_FMA(x2, p[12], p[10]);
+    const double s1 = GM_FMA(x2, kSc_s3, kSc_s2);
     const double x7 = x3 * x2;
-    const double s = GM_FMA(x3, p[8], x);
+    const double s = GM_FMA(x3, kSc_s1, x);
     return (float)GM_FMA(x7, s1, s);
   }
   const double x4 = x2 * x2;
-  const double c2 = GM_FMA(x2, p[13], p[11]);
-  const double c1 = GM_FMA(x2, p[7], p[6]);
+  const double c2 = GM_FMA(x2, kSc_c4, kSc_c3);
+  const double c1 = GM_FMA(x2, kSc_c1, kSc_c0);
   const double x6 = x4 * x2;
-  const double c = GM_FMA(x4, p[9], c1);
-  return (float)GM_FMA(x6, c2, c);
+  const double c = GM_FMA(x4, kSc_c2, c1);
+  const float r = (float)GM_FMA(x6, c2, c);
+  return neg_cos ? -r : r;
 }
+
+// sign of sine in quadrant q = 0..3: {1, -1, -1, 1}
+GM_FN double quadrant_sign(int q) { return ((q + 1) & 2) ? -1.0 : 1.0; }
 
 // reduce_fast: n = round(x * 2/pi) (from x * 2^24 * 2/pi), x - n pi/2
 GM_FN double reduce_fast(double x, int& n) {
-  const double r = x * kSincosf[0][4];
+  const double r = x * kSc_hpi_inv;
   n = ((int32_t)r + 0x800000) >> 24;
-  return GM_FMA(-(double)n, kSincosf[0][5], x);
+  return GM_FMA(-(double)n, kSc_hpi, x);
 }
 
 // reduce_large: |y| >= 120, Payne-Hanek with 4/pi to 192 bits; x in
@@ -204,23 +209,19 @@ GM_FN float sinf_(float y) {
   double x = y;
   if (a < (top12(0x1.921fb6p-1f) & 0x7ff)) {  // |y| < pi/4
     if (a < (top12(0x1p-12f) & 0x7ff)) return y;
-    return sinf_poly(x, x * x, 0, 0);
+    return sinf_poly(x, x * x, false, 0);
   }
   if (a < (top12(120.0f) & 0x7ff)) {
     int n;
     x = reduce_fast(x, n);
-    const double s = kSincosf[0][n & 3];
-    const int t = (n & 2) ? 1 : 0;
-    return sinf_poly(x * s, x * x, t, n);
+    return sinf_poly(x * quadrant_sign(n & 3), x * x, (n & 2) != 0, n);
   }
   if (a < (top12(INFINITY) & 0x7ff)) {
     const uint32_t xi = asuint(y);
     const int sign = xi >> 31;
     int n;
     x = reduce_large(xi, n);
-    const double s = kSincosf[0][(n + sign) & 3];
-    const int t = ((n + sign) & 2) ? 1 : 0;
-    return sinf_poly(x * s, x * x, t, n);
+    return sinf_poly(x * quadrant_sign((n + sign) & 3), x * x, ((n + sign) & 2) != 0, n);
   }
   return y - y;  // inf / nan
 }
@@ -230,23 +231,19 @@ GM_FN float cosf_(float y) {
   double x = y;
   if (a < (top12(0x1.921fb6p-1f) & 0x7ff)) {
     if (a < (top12(0x1p-12f) & 0x7ff)) return 1.0f;
-    return sinf_poly(x, x * x, 0, 1);
+    return sinf_poly(x, x * x, false, 1);
   }
   if (a < (top12(120.0f) & 0x7ff)) {
     int n;
     x = reduce_fast(x, n);
-    const double s = kSincosf[0][n & 3];
-    const int t = (n & 2) ? 1 : 0;
-    return sinf_poly(x * s, x * x, t, n ^ 1);
+    return sinf_poly(x * quadrant_sign(n & 3), x * x, (n & 2) != 0, n ^ 1);
   }
   if (a < (top12(INFINITY) & 0x7ff)) {
     const uint32_t xi = asuint(y);
     const int sign = xi >> 31;
     int n;
     x = reduce_large(xi, n);
-    const double s = kSincosf[0][(n + sign) & 3];
-    const int t = ((n + sign) & 2) ? 1 : 0;
-    return sinf_poly(x * s, x * x, t, n ^ 1);
+    return sinf_poly(x * quadrant_sign((n + sign) & 3), x * x, ((n + sign) & 2) != 0, n ^ 1);
   }
   return y - y;  // inf / nan
 }

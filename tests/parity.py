@@ -11,6 +11,7 @@ import numpy as np
 REL_TOL = 1e-3
 ABS_TOL = 1e-6
 MIN_MATCH = 0.99
+MIN_BITEXACT = 0.999  # golden renders: measured 1.0 on the MI355X
 
 
 def compare_paths(got: np.ndarray, want: np.ndarray) -> dict:
