@@ -1691,14 +1691,16 @@ SRR_D bool shade_one(const SceneView& S, const PathState& P, int p, int max_dept
 constexpr int kPathsBlock = 256;
 constexpr unsigned long long kPoolChunk = 64;  // path indices a wave takes per cursor atomic
 
-template <bool MEDIA, bool ALLFAM, int MINB, bool TIMED = false>
+template <bool MEDIA, bool ALLFAM, int MINB, bool TIMED = false, bool WL = true>
 __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathWork W) {
   // TIMED (diagnostics): per-wave cycles in refill / world hit (mesh part) / record+scatter / fold
   uint64_t tp[6] = {0, 0, 0, 0, 0, 0};
   uint64_t it = 0;
   SceneView S = S0;
-  constexpr int TR = TR_BVH4_PRUNE | TR_WL;
-  {
+  // WL: world tables staged in LDS (they fit in kWorldLdsBytes); otherwise read
+  // from global memory (large object lists, e.g. random_scene's ~490 spheres)
+  constexpr int TR = TR_BVH4_PRUNE | (WL ? TR_WL : 0);
+  if constexpr (WL) {
     __shared__ uint4 s_world[kWorldLdsBytes / 16];
     for (int i = threadIdx.x; i < S0.world_words; i += blockDim.x) s_world[i] = S0.world_blob[i];
     __syncthreads();
@@ -1796,7 +1798,7 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
     }
     if (g >= 0) {
       ++prays;
-      const WorldHit w = world_hit<MEDIA, TIMED ? (TR_BVH4_TIMED | TR_WL) : TR>(S, r, rng, cx);
+      const WorldHit w = world_hit<MEDIA, TIMED ? (TR_BVH4_TIMED | (WL ? TR_WL : 0)) : TR>(S, r, rng, cx);
       if (TIMED) {
         const uint64_t t = __builtin_amdgcn_s_memtime();
         tp[1] += t - tq - cx.mesh_cycles;
@@ -2289,6 +2291,19 @@ int paths_lanes_per_device(const SceneView& S, int device) {
 void launch_paths(const SceneView& S, const PathWork& W, int all_families, hipStream_t st) {
   const int blocks = W.lanes / dev::kPathsBlock;
   static const bool timed = getenv("SRR_PATHS_TIMING") != nullptr;
+  if (S.world_words * 16 > dev::kWorldLdsBytes) {  // world tables too large for LDS: global reads
+#define SRR_LAUNCH_PATHS_G(M, A) \
+  hipLaunchKernelGGL((dev::k_paths<M, A, 4, false, false>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W)
+    if (S.has_media) {
+      if (all_families) SRR_LAUNCH_PATHS_G(true, true);
+      else SRR_LAUNCH_PATHS_G(true, false);
+    } else {
+      if (all_families) SRR_LAUNCH_PATHS_G(false, true);
+      else SRR_LAUNCH_PATHS_G(false, false);
+    }
+#undef SRR_LAUNCH_PATHS_G
+    return;
+  }
 #define SRR_LAUNCH_PATHS(M, A, B)                                                                      \
   if (timed) hipLaunchKernelGGL((dev::k_paths<M, A, 4, true>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W); \
   else hipLaunchKernelGGL((dev::k_paths<M, A, B>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W)

@@ -324,9 +324,9 @@ int render_device(srr_renderer* r, const srr_params* p, const int32_t* pix, int6
     return e && !strcmp(e, "wave");
   }();
   const bool wave_engine = wave_env || (p->flags & SRR_FLAG_WAVEFRONT);
-  // the path engine stages the world tables in LDS (kernels.hip kWorldLdsBytes)
-  const bool fits = (size_t)r->view.world_words * 16 <= (size_t)kPathsWorldLdsBytes;
-  if (!wave_engine && fits && !(p->flags & SRR_FLAG_COUNT_VISITS))
+  // the path engine stages the world tables in LDS when they fit
+  // (kernels.hip kWorldLdsBytes) and reads them from global memory otherwise
+  if (!wave_engine && !(p->flags & SRR_FLAG_COUNT_VISITS))
     return render_paths(r, p, pix, npix, d_mean, stats, err);
   RCHK(hipSetDevice(r->device));
   const bool keep = (p->flags & SRR_FLAG_KEEP_PATHS) != 0;

@@ -42,6 +42,9 @@ def test_paths_match_reference(name, engine):
     print(f"{name}: {pc} rays_eq={rays_eq:.5f} world_rays={out['stats']['world_rays']} "
           f"(ref {m['world_rays']}) img={ic}")
     assert pc["match"] >= parity.MIN_MATCH, pc
+    # the device rounds like the reference (correctly rounded sqrt, glibc's float
+    # libm algorithms): paths are bit-identical, not just within tolerance
+    assert pc["bitexact"] >= parity.MIN_BITEXACT, pc
     assert rays_eq >= parity.MIN_MATCH
     assert abs(out["stats"]["world_rays"] - m["world_rays"]) <= 0.01 * m["world_rays"]
     assert ic["mean_rel"] <= 0.005, ic
