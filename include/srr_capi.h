@@ -152,6 +152,10 @@ typedef struct srr_params {
 #define SRR_FLAG_COUNT_VISITS 4   /* count mesh box / triangle tests (slower)    */
 #define SRR_FLAG_WAVEFRONT 8      /* use the wavefront engine (per-bounce kernels) */
                                   /* instead of the path-resident persistent one  */
+#define SRR_FLAG_CONTINUE 16      /* progressive rendering: add this render's      */
+                                  /* samples to the renderer's per-pixel running   */
+                                  /* sums (set sample_begin to the samples already */
+                                  /* in them); the mean covers all of them         */
 
 typedef struct srr_stats {
   int64_t world_rays;   /* world->hit calls (the metric's samples)             */
@@ -182,6 +186,13 @@ int srr_render_device(srr_renderer* r, const srr_params* p, float* d_mean, srr_s
  * (the whole image when shard_count <= 1) as mean radiance (npix*3, may be NULL)
  * and 8-bit tone-mapped rgb8 (npix*3, Raytracing_n.cpp:850-867, may be NULL). */
 int srr_render(srr_renderer* r, const srr_params* p, float* mean, unsigned char* rgb8, srr_stats* stats);
+/* Progressive rendering with resume: the renderer's per-pixel running sums
+ * (3 floats per shard pixel, in srr_shard_pixels order) and the samples per pixel
+ * they hold.  get: sums may be NULL to query npix / samples.  set: restores a saved
+ * state, after which renders with SRR_FLAG_CONTINUE and sample_begin = samples
+ * continue it (bitwise the image of one render of all the samples). */
+int srr_accum_get(srr_renderer* r, float* sums, int64_t* npix, int64_t* samples);
+int srr_accum_set(srr_renderer* r, const float* sums, int64_t npix, int64_t samples);
 /* After a render with SRR_FLAG_KEEP_PATHS: per-path raw radiance (before
  * de_nan) and world-ray counts, [n_shard_pixels][spp]. */
 int srr_copy_paths(srr_renderer* r, float* radiance, unsigned char* rays);

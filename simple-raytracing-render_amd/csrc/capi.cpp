@@ -345,6 +345,36 @@ int srr_render(srr_renderer* r, const srr_params* p, float* mean, unsigned char*
   return 0;
 }
 
+int srr_accum_get(srr_renderer* r, float* sums, int64_t* npix, int64_t* samples) {
+  if (!r) return fail(SRR_EINVAL, "null renderer");
+  if (npix) *npix = r->acc_npix;
+  if (samples) *samples = r->acc_samples;
+  if (sums && r->acc_npix) {
+    HIPCHK(hipSetDevice(r->device));
+    HIPCHK(hipMemcpy(sums, r->acc, 3 * r->acc_npix * sizeof(float), hipMemcpyDeviceToHost));
+  }
+  return 0;
+}
+
+int srr_accum_set(srr_renderer* r, const float* sums, int64_t npix, int64_t samples) {
+  if (!r || !sums || npix <= 0 || samples < 0) return fail(SRR_EINVAL, "bad accumulator state");
+  HIPCHK(hipSetDevice(r->device));
+  if ((size_t)npix > r->pix_cap) {
+    (void)hipFree(r->pixels);
+    (void)hipFree(r->acc);
+    r->pixels = nullptr;
+    r->acc = nullptr;
+    r->pix_cap = 0;
+    HIPCHK(hipMalloc((void**)&r->pixels, npix * sizeof(int32_t)));
+    HIPCHK(hipMalloc((void**)&r->acc, 3 * npix * sizeof(float)));
+    r->pix_cap = npix;
+  }
+  HIPCHK(hipMemcpy(r->acc, sums, 3 * npix * sizeof(float), hipMemcpyHostToDevice));
+  r->acc_npix = npix;
+  r->acc_samples = samples;
+  return 0;
+}
+
 int srr_copy_paths(srr_renderer* r, float* radiance, unsigned char* rays) {
   if (!r || !r->raw_all) return fail(SRR_EINVAL, "render with SRR_FLAG_KEEP_PATHS first");
   HIPCHK(hipSetDevice(r->device));

@@ -184,6 +184,23 @@ static int ensure_lane(Lane& L, size_t n, int depth, bool keep, std::string& err
   return 0;
 }
 
+// Per-pixel running sums: zeroed by a render without SRR_FLAG_CONTINUE; a render
+// with it adds its samples to them, so consecutive sample ranges accumulate in
+// sample order -- bitwise the sums of one render of all of them.
+static int begin_accum(srr_renderer* r, const srr_params* p, int64_t npix, hipStream_t st, std::string& err) {
+  if (p->flags & SRR_FLAG_CONTINUE) {
+    if (r->acc_npix != npix) {
+      err = "SRR_FLAG_CONTINUE: no running sums for this shard (render without the flag or srr_accum_set first)";
+      return SRR_EINVAL;
+    }
+    return 0;
+  }
+  RCHK(hipMemsetAsync(r->acc, 0, 3 * npix * sizeof(float), st));
+  r->acc_npix = npix;
+  r->acc_samples = 0;
+  return 0;
+}
+
 // Path-resident engine (kernels.hip k_paths): one persistent kernel per window
 // of samples; samples land in a [pixel][sample] buffer that k_accumulate_window
 // sums per pixel in sample order, so the image is bitwise the wavefront engine's.
@@ -252,7 +269,10 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
   }
   if (!r->pw_ctr) RCHK(hipMalloc((void**)&r->pw_ctr, 16 * sizeof(unsigned long long)));
   RCHK(hipMemsetAsync(r->pw_ctr, 0, 16 * sizeof(unsigned long long), st));
-  RCHK(hipMemsetAsync(r->acc, 0, 3 * npix * sizeof(float), st));
+  {
+    const int rc = begin_accum(r, p, npix, st, err);
+    if (rc < 0) return rc;
+  }
   const bool all_fam = !r->diffuse_only;
   RCHK(hipEventRecord(r->ev_beg, st));
   double kernel_ms = 0;
@@ -290,7 +310,8 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
     kernel_ms += ms;
     s.trace_launches += 1;
   }
-  launch_finish(r->acc, d_mean, npix, p->spp, st);
+  r->acc_samples += p->spp;
+  launch_finish(r->acc, d_mean, npix, (int)r->acc_samples, st);
   RCHK(hipEventRecord(r->ev_end, st));
   RCHK(hipStreamSynchronize(st));
   RCHK(hipGetLastError());
@@ -410,7 +431,10 @@ int render_device(srr_renderer* r, const srr_params* p, const int32_t* pix, int6
     if (rc < 0) return rc;
   }
   RCHK(hipDeviceSynchronize());
-  RCHK(hipMemsetAsync(r->acc, 0, 3 * npix * sizeof(float), ast));
+  {
+    const int rc = begin_accum(r, p, npix, ast, err);
+    if (rc < 0) return rc;
+  }
   RCHK(hipEventRecord(r->ev_beg, ast));
   for (int l = 0; l < lanes; ++l) {
     Lane& L = r->lanes[l];
@@ -531,7 +555,8 @@ int render_device(srr_renderer* r, const srr_params* p, const int32_t* pix, int6
     }
     if (!progress) std::this_thread::yield();
   }
-  launch_finish(r->acc, d_mean, npix, p->spp, ast);
+  r->acc_samples += p->spp;
+  launch_finish(r->acc, d_mean, npix, (int)r->acc_samples, ast);
   RCHK(hipEventRecord(r->ev_end, ast));
   RCHK(hipStreamSynchronize(ast));
   RCHK(hipGetLastError());

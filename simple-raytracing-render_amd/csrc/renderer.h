@@ -58,6 +58,8 @@ struct srr_renderer {
   hipEvent_t ev_beg = nullptr, ev_end = nullptr;
   // frame buffers
   float* acc = nullptr;
+  int64_t acc_npix = 0;     // pixels the running sums cover (SRR_FLAG_CONTINUE)
+  int64_t acc_samples = 0;  // samples per pixel accumulated in them
   unsigned long long* visits = nullptr;  // SRR_FLAG_COUNT_VISITS counters (3)
   // path-resident engine (render_paths)
   int pw_lanes = 0;

@@ -17,6 +17,7 @@ FLAG_SORT_MATERIALS = 1
 FLAG_KEEP_PATHS = 2
 FLAG_COUNT_VISITS = 4
 FLAG_WAVEFRONT = 8
+FLAG_CONTINUE = 16
 
 
 class SrrError(RuntimeError):
@@ -68,6 +69,9 @@ def lib():
         L.srr_image_free.argtypes = [u8p]
         L.srr_image_free.restype = None
         L.srr_write_png.argtypes = [cp, ip, ip, vp]
+        i64p = ctypes.POINTER(ctypes.c_int64)
+        L.srr_accum_get.argtypes = [vp, vp, i64p, i64p]
+        L.srr_accum_set.argtypes = [vp, vp, ctypes.c_int64, ctypes.c_int64]
         _LIB = L
     return _LIB
 
@@ -107,6 +111,7 @@ class Scene:
         h = ctypes.c_void_p()
         _check(lib().srr_scene_from_text(text.encode(), ctypes.byref(h)))
         self.h = h
+        self.text = text
 
     def __del__(self):
         if getattr(self, "h", None):
