@@ -1077,6 +1077,10 @@ struct Bsdf {
   float A, B;      // orennayar
   Beck dist;       // beckmann
   float beck_pdf;  // beckmann_pdf::pdf_value, set by generate (starts 0)
+  // value()'s terms that depend only on the incoming direction, computed once per
+  // bounce (bsdf_prepare) instead of once per resampling iteration
+  float co;        // cosine_pdf: dot(unit_vector(wo), n)
+  V3 lo;           // onrennayar_pdf: local unit(-wo)
 };
 
 SRR_D V3 to_local_unit(const Onb& b, V3 d) {
@@ -1106,16 +1110,24 @@ SRR_D V3 bsdf_generate(Bsdf& f, V3 wo, Rng& rng) {
 }
 
 template <bool BECK>
-SRR_D float bsdf_value(const Bsdf& f, V3 wo, V3 wi) {
+SRR_D void bsdf_prepare(Bsdf& f, V3 wo) {
+  if (BECK) return;
+  if (f.kind == MAT_LAMBERTIAN) f.co = dot(unit_vector(wo), f.n);
+  else f.lo = to_local_unit(f.uvw, -wo);
+}
+
+template <bool BECK>
+SRR_D float bsdf_value(const Bsdf& f, V3 wo, V3 wi) {  // after bsdf_prepare(f, wo)
+  (void)wo;
   if (BECK) return f.beck_pdf;
   if (f.kind == MAT_LAMBERTIAN) {  // pdf.h:33-46
-    float co = dot(unit_vector(wo), f.n);
+    const float co = f.co;
     float ci = dot(unit_vector(wi), f.n);
     if (ci * co < 0) return fabsf(ci) / kPi;
     return 0;
   }
   // onrennayar_pdf::value (pdf.h:64-101)
-  V3 lo = to_local_unit(f.uvw, -wo);
+  const V3 lo = f.lo;
   V3 li = to_local_unit(f.uvw, wi);
   float sinThetaI = SinTheta(li), sinThetaO = SinTheta(lo);
   float maxCos = 0;
@@ -1620,6 +1632,7 @@ SRR_D void scatter(const SceneView& S, const DMat& M, V3 rdir, float rtime, V3 h
     f.dist.ax = M.p[0];
     f.dist.ay = M.p[1];
     f.beck_pdf = 0;
+    bsdf_prepare<F == FAM_BECK>(f, rdir);
     float pdf_val = 0;
     if (S.n_lights > 0) {
       (void)drand(rng);  // mixture_pdf ctor (pdf.h:175)
@@ -2054,6 +2067,7 @@ __global__ void k_kat(int kind, int n, int w, float* rec, const float* aux, cons
       f.A = a[0];
       f.B = a[1];
       const V3 wo = kat3(r + 4);
+      bsdf_prepare<false>(f, wo);
       Rng rng{kat_lcg(r + 7), 0};
       const V3 d = bsdf_generate<false>(f, wo, rng);
       r[9] = a[0];
@@ -2291,7 +2305,8 @@ int paths_lanes_per_device(const SceneView& S, int device) {
 void launch_paths(const SceneView& S, const PathWork& W, int all_families, hipStream_t st) {
   const int blocks = W.lanes / dev::kPathsBlock;
   static const bool timed = getenv("SRR_PATHS_TIMING") != nullptr;
-  if (S.world_words * 16 > dev::kWorldLdsBytes) {  // world tables too large for LDS: global reads
+  static const bool force_global = getenv("SRR_WORLD_GLOBAL") != nullptr;  // A/B diagnostics
+  if (force_global || S.world_words * 16 > dev::kWorldLdsBytes) {  // world tables too large for LDS: global reads
 #define SRR_LAUNCH_PATHS_G(M, A) \
   hipLaunchKernelGGL((dev::k_paths<M, A, 4, false, false>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W)
     if (S.has_media) {
