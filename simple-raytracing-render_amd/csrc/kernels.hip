@@ -1936,6 +1936,50 @@ __global__ void __launch_bounds__(256) k_accumulate_window(const float* sample, 
   acc[a + 2] = cz;
 }
 
+// The same sums with 16-byte loads, for windows of a multiple of kAccChunk samples:
+// a pixel's chunk is 12 contiguous float4 (16-byte aligned), so a block fetches
+// its 256 x 16 samples with 12 float4 loads per thread (no per-element division).
+__global__ void __launch_bounds__(256) k_accumulate_window16(const float4* sample4, int npix, int spp_w, float* acc) {
+  __shared__ float tile[256 * (3 * kAccChunk + 1)];
+  constexpr int kQ = 3 * kAccChunk / 4;  // float4 per pixel chunk
+  const int p0 = blockIdx.x * 256;
+  const int lp = p0 + threadIdx.x;
+  const int np = min(256, npix - p0);
+  float cx = 0, cy = 0, cz = 0;
+  if (lp < npix) {
+    cx = acc[3 * (size_t)lp];
+    cy = acc[3 * (size_t)lp + 1];
+    cz = acc[3 * (size_t)lp + 2];
+  }
+  for (int s0 = 0; s0 < spp_w; s0 += kAccChunk) {
+    for (int i = threadIdx.x; i < np * kQ; i += 256) {
+      const int px = i / kQ, f4 = i - px * kQ;
+      const float4 v = ntl(&sample4[((size_t)(p0 + px) * spp_w + s0) * 3 / 4 + f4]);
+      float* d = &tile[px * (3 * kAccChunk + 1) + 4 * f4];
+      d[0] = v.x;
+      d[1] = v.y;
+      d[2] = v.z;
+      d[3] = v.w;
+    }
+    __syncthreads();
+    if (lp < npix) {
+      const float* t = &tile[threadIdx.x * (3 * kAccChunk + 1)];
+#pragma unroll
+      for (int k = 0; k < kAccChunk; ++k) {
+        cx += t[3 * k];
+        cy += t[3 * k + 1];
+        cz += t[3 * k + 2];
+      }
+    }
+    __syncthreads();
+  }
+  if (lp >= npix) return;
+  const size_t a = 3 * (size_t)lp;
+  acc[a] = cx;
+  acc[a + 1] = cy;
+  acc[a + 2] = cz;
+}
+
 constexpr int kMaxRegions = 8;
 
 // Grid-stride over family F's list (sized on the device: no host readback);
@@ -2347,7 +2391,12 @@ int launch_kat(int kind, int n, int w, float* d_rec, const float* d_aux, const D
 }
 
 void launch_accumulate_window(const float* sample, int npix, int spp_w, float* acc, hipStream_t st) {
-  hipLaunchKernelGGL(dev::k_accumulate_window, dim3((npix + 255) / 256), dim3(256), 0, st, sample, npix, spp_w, acc);
+  static const bool scalar = getenv("SRR_ACC_SCALAR") != nullptr;  // A/B diagnostics
+  if (spp_w % dev::kAccChunk == 0 && ((uintptr_t)sample & 15) == 0 && !scalar)
+    hipLaunchKernelGGL(dev::k_accumulate_window16, dim3((npix + 255) / 256), dim3(256), 0, st, (const float4*)sample,
+                       npix, spp_w, acc);
+  else
+    hipLaunchKernelGGL(dev::k_accumulate_window, dim3((npix + 255) / 256), dim3(256), 0, st, sample, npix, spp_w, acc);
 }
 
 }  // namespace srr
