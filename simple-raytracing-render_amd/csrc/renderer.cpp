@@ -256,7 +256,14 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
   // sample window: all pixels x W samples, buffer within SRR_WINDOW_MB (default 8192)
   size_t budget = (size_t)8192 << 20;
   if (const char* e = getenv("SRR_WINDOW_MB")) budget = (size_t)std::max(1, atoi(e)) << 20;
-  const int W = (int)std::max<int64_t>(1, std::min<int64_t>(p->spp, (int64_t)(budget / (12 * (size_t)npix))));
+  // (k_paths numbers a window's paths in 32 bits: npix * W < 2^31)
+  const int64_t w_max = std::max<int64_t>(1, (((int64_t)1 << 31) - 1) / std::max<int64_t>(1, npix));
+  const int W = (int)std::max<int64_t>(
+      1, std::min<int64_t>(std::min<int64_t>(p->spp, w_max), (int64_t)(budget / (12 * (size_t)npix))));
+  if ((int64_t)npix * W >= ((int64_t)1 << 31)) {
+    err = "frame too large for one sample window (npix >= 2^31)";
+    return SRR_EINVAL;
+  }
   const size_t win_paths = (size_t)npix * W;
   if (win_paths > r->pw_sample_cap) {
     (void)hipFree(r->pw_sample);
