@@ -45,9 +45,14 @@ struct DXform {  // one instance wrapper (hitable.h:35-203, aarect.h:149-171)
   float a, b, c;  // translate: offset; rotate: sin, cos
 };
 
+// DObj::xf_count: moving transforms (translate / rotate) in the low bits, and
+// kXfFlipBit when an odd number of flip_normals wrap the object
+constexpr int32_t kXfFlipBit = 1 << 30;
+constexpr int32_t kXfCountMask = 0xFFFF;
+
 struct DObj {
   int32_t kind;
-  int32_t xf_begin, xf_count;  // chain, outermost first
+  int32_t xf_begin, xf_count;  // chain, outermost first (xf_count: see kXfFlipBit)
   int32_t idx;                 // row in the kind's table
 };
 

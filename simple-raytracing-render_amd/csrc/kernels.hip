@@ -379,7 +379,8 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
 // 180-188; flip leaves the ray alone)
 template <int TR = 0>
 SRR_D Ray chain_in(const SceneView& S, const DObj& ob, Ray r) {
-  for (int k = 0; k < ob.xf_count; ++k) {
+  const int n = ob.xf_count & kXfCountMask;
+  for (int k = 0; k < n; ++k) {
     DXform x = wload<TR>(S.xforms, ob.xf_begin + k);
     if (x.kind == XF_TRANSLATE) r.o = r.o - v3(x.a, x.b, x.c);
     else if (x.kind == XF_ROTY || x.kind == XF_ROTX) {
@@ -399,10 +400,9 @@ SRR_D Ray chain_in(const SceneView& S, const DObj& ob, Ray r) {
 
 // ...and the hit record coming out, innermost first
 SRR_D void chain_out(const SceneView& S, const DObj& ob, V3& p, V3& n) {
-  for (int k = ob.xf_count - 1; k >= 0; --k) {
+  for (int k = (ob.xf_count & kXfCountMask) - 1; k >= 0; --k) {
     DXform x = S.xforms[ob.xf_begin + k];
-    if (x.kind == XF_FLIP) n = -n;
-    else if (x.kind == XF_TRANSLATE) p = p + v3(x.a, x.b, x.c);
+    if (x.kind == XF_TRANSLATE) p = p + v3(x.a, x.b, x.c);
     else {
       int ia = x.kind == XF_ROTY ? 0 : 1;
       float s = x.a, c = x.b;
@@ -415,6 +415,7 @@ SRR_D void chain_out(const SceneView& S, const DObj& ob, V3& p, V3& n) {
       n = nn;
     }
   }
+  if (ob.xf_count & kXfFlipBit) n = -n;  // flip_normals (aarect.h:149-171), exact in any order
 }
 
 struct ObjHit {

@@ -877,10 +877,19 @@ struct Flattener {
   bool walk(int h, std::vector<DXform> ch, std::vector<DObj>& out, bool in_medium) {
     const HObj& o = S.obj[h];
     auto emit = [&](int kind, int idx) {
+      // flip_normals only negates the normal, which commutes with the rotations
+      // and is untouched by translations: the chain keeps the moving transforms
+      // and the flips become one parity bit (kXfFlipBit), applied last on the way out
+      std::vector<DXform> moving;
+      int flips = 0;
+      for (const DXform& x : ch) {
+        if (x.kind == XF_FLIP) ++flips;
+        else moving.push_back(x);
+      }
       DObj d;
       d.kind = kind;
-      d.xf_begin = chain_push(ch);
-      d.xf_count = (int)ch.size();
+      d.xf_begin = chain_push(moving);
+      d.xf_count = (int)moving.size() | ((flips & 1) ? kXfFlipBit : 0);
       d.idx = idx;
       out.push_back(d);
     };
