@@ -2,12 +2,12 @@
 //
 // The reference is compiled C++ on x86-64 (no FMA) linked to glibc's libm.  To
 // track it on gfx950:
-//  * kernels are compiled with -ffp-contract=off (no FMA contraction), and HIP's
-//    default correctly rounded f32 division / sqrt;
+//  * kernels are compiled with -ffp-contract=off (no FMA contraction) and HIP's
+//    default correctly rounded f32 division; f32 sqrt is made correctly rounded
+//    here (rsqrt_exact);
 //  * the reference's float libm calls run glibc's own algorithms and tables
-//    (glibc_mathf.h: sinf, cosf, expf, logf, powf, acosf -- bit-exact with the
-//    host's libm); asinf and atan2f (sphere uv only) are evaluated in double and
-//    rounded once, which matches glibc except in the last bit of rare inputs;
+//    (glibc_mathf.h: sinf, cosf, expf, logf, powf, acosf, asinf, atan2f --
+//    bit-exact with the host's libm);
 //  * double libm calls (sin/cos/log/pow of double) use the device double libm.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -53,6 +53,8 @@ SRR_D float rexp(float x) { return gm::expf_(x); }
 SRR_D float rlog(float x) { return gm::logf_(x); }
 SRR_D float rpow(float x, float y) { return gm::powf_(x, y); }
 SRR_D float racos(float x) { return gm::acosf_(x); }
+SRR_D float rasin(float x) { return gm::asinf_(x); }
+SRR_D float ratan2(float y, float x) { return gm::atan2f_(y, x); }
 #else
 SRR_D float rsin(float x) { return (float)::sin((double)x); }
 SRR_D float rcos(float x) { return (float)::cos((double)x); }
@@ -60,9 +62,9 @@ SRR_D float rexp(float x) { return (float)::exp((double)x); }
 SRR_D float rlog(float x) { return (float)::log((double)x); }
 SRR_D float rpow(float x, float y) { return (float)::pow((double)x, (double)y); }
 SRR_D float racos(float x) { return (float)::acos((double)x); }
-#endif
 SRR_D float rasin(float x) { return (float)::asin((double)x); }
 SRR_D float ratan2(float y, float x) { return (float)::atan2((double)y, (double)x); }
+#endif
 SRR_D float rdiv(float a, float b) { return __fdiv_rn(a, b); }
 
 static constexpr double kPi = 3.14159265358979323846;  // mathf.h:10

@@ -13,9 +13,9 @@
 // with the fused multiply-adds of glibc's x86-64 FMA variants (selected on any
 // CPU with FMA, e.g. e_expf-fma.c), so the device returns the host's float bit
 // for bit.  tools/check_glibc_mathf.cpp compares them with libm over every float
-// input (expf, logf, sinf, cosf, acosf) and over sampled (x, y) pairs (powf):
+// input (expf, logf, sinf, cosf, acosf, asinf, atanf) and over sampled pairs (powf, atan2f):
 // all bit-exact except expf at 2 of the 2^32 inputs (1 ulp, |x| > 32).  acosf
-// is glibc's fdlibm float routine, restated.
+// asinf / atanf / atan2f are glibc's fdlibm float routines, restated.
 //
 // Special powf operands (zero / inf / nan / negative or subnormal x, results
 // beyond 2^+-126) take the double-precision route; the reference never meets them.
@@ -284,6 +284,105 @@ GM_FN float acosf_(float x) {
   const float r = p / q;
   const float w = r * s + c;
   return 2.0f * (df + w);
+}
+
+// s_atanf.c / e_atan2f.c / e_asinf.c: glibc's fdlibm float routines (float
+// arithmetic), restated; used by get_sphere_uv (hitable.h:10-15)
+GM_FN float atanf_(float x) {
+  const float atanhi[4] = {4.6364760399e-01f, 7.8539812565e-01f, 9.8279368877e-01f, 1.5707962513e+00f};
+  const float atanlo[4] = {5.0121582440e-09f, 3.7748947079e-08f, 3.4473217170e-08f, 7.5497894159e-08f};
+  const float a0 = 3.3333334327e-01f, a1 = -2.0000000298e-01f, a2 = 1.4285714924e-01f, a3 = -1.1111110449e-01f,
+              a4 = 9.0908870101e-02f, a5 = -7.6918758452e-02f, a6 = 6.6610731184e-02f, a7 = -5.8335702866e-02f,
+              a8 = 4.9768779427e-02f, a9 = -3.6531571299e-02f, a10 = 1.6285819933e-02f;
+  const int32_t hx = (int32_t)asuint(x), ix = hx & 0x7fffffff;
+  int id;
+  if (ix >= 0x4c000000) {  // |x| >= 2^25
+    if (ix > 0x7f800000) return x + x;
+    return hx > 0 ? atanhi[3] + atanlo[3] : -atanhi[3] - atanlo[3];
+  }
+  if (ix < 0x3ee00000) {  // |x| < 0.4375
+    if (ix < 0x31000000) return x;
+    id = -1;
+  } else {
+    x = fabsf(x);
+    if (ix < 0x3f980000) {
+      if (ix < 0x3f300000) id = 0, x = (2.0f * x - 1.0f) / (2.0f + x);
+      else id = 1, x = (x - 1.0f) / (x + 1.0f);
+    } else {
+      if (ix < 0x401c0000) id = 2, x = (x - 1.5f) / (1.0f + 1.5f * x);
+      else id = 3, x = -1.0f / x;
+    }
+  }
+  const float z = x * x, w = z * z;
+  const float s1 = z * (a0 + w * (a2 + w * (a4 + w * (a6 + w * (a8 + w * a10)))));
+  const float s2 = w * (a1 + w * (a3 + w * (a5 + w * (a7 + w * a9))));
+  if (id < 0) return x - x * (s1 + s2);
+  const float zz = atanhi[id] - ((x * (s1 + s2) - atanlo[id]) - x);
+  return hx < 0 ? -zz : zz;
+}
+
+GM_FN float atan2f_(float y, float x) {
+  const float tiny = 1.0e-30f, pi_o_4 = 7.8539818525e-01f, pi_o_2 = 1.5707963705e+00f, pi = 3.1415927410e+00f,
+              pi_lo = -8.7422776573e-08f;
+  const int32_t hx = (int32_t)asuint(x), ix = hx & 0x7fffffff, hy = (int32_t)asuint(y), iy = hy & 0x7fffffff;
+  if (ix > 0x7f800000 || iy > 0x7f800000) return x + y;
+  if (hx == 0x3f800000) return atanf_(y);
+  const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);  // 2 * sign(x) + sign(y)
+  if (iy == 0) return m <= 1 ? y : (m == 2 ? pi + tiny : -pi - tiny);
+  if (ix == 0) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+  if (ix == 0x7f800000) {
+    if (iy == 0x7f800000) {
+      const float q[4] = {pi_o_4 + tiny, -pi_o_4 - tiny, 3.0f * pi_o_4 + tiny, -3.0f * pi_o_4 - tiny};
+      return q[m];
+    }
+    const float q[4] = {0.0f, -0.0f, pi + tiny, -pi - tiny};
+    return q[m];
+  }
+  if (iy == 0x7f800000) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+  const int k = (iy - ix) >> 23;
+  float z;
+  if (k > 60) z = pi_o_2 + 0.5f * pi_lo;
+  else if (hx < 0 && k < -60) z = 0.0f;
+  else z = atanf_(fabsf(y / x));
+  switch (m) {
+    case 0: return z;
+    case 1: return -z;
+    case 2: return pi - (z - pi_lo);
+    default: return (z - pi_lo) - pi;
+  }
+}
+
+GM_FN float asinf_(float x) {
+  const float one = 1.0f, huge = 1.000e+30f, pio2_hi = 1.57079637050628662109375f, pio2_lo = -4.37113900018624283e-8f,
+              pio4_hi = 0.785398185253143310546875f, p0 = 1.666675248e-1f, p1 = 7.495297643e-2f,
+              p2 = 4.547037598e-2f, p3 = 2.417951451e-2f, p4 = 4.216630880e-2f;
+  const int32_t hx = (int32_t)asuint(x), ix = hx & 0x7fffffff;
+  if (ix == 0x3f800000) return x * pio2_hi + x * pio2_lo;
+  if (ix > 0x3f800000) return (x - x) / (x - x);
+  if (ix < 0x3f000000) {  // |x| < 0.5
+    if (ix < 0x32000000) {
+      if (huge + x > one) return x;
+    } else {
+      const float t = x * x;
+      const float w = t * (p0 + t * (p1 + t * (p2 + t * (p3 + t * p4))));
+      return x + x * w;
+    }
+  }
+  float w = one - fabsf(x);
+  float t = w * 0.5f;
+  float p = t * (p0 + t * (p1 + t * (p2 + t * (p3 + t * p4))));
+  const float s = GM_SQRTF(t);
+  if (ix >= 0x3F79999A) {  // |x| > 0.975
+    t = pio2_hi - (2.0f * (s + s * p) - pio2_lo);
+  } else {
+    w = asfloat(asuint(s) & 0xfffff000u);
+    const float c = (t - w * w) / (s + w);
+    const float r = p;
+    p = 2.0f * s * r - (pio2_lo - 2.0f * c);
+    const float q = pio4_hi - 2.0f * w;
+    t = pio4_hi - (p - q);
+  }
+  return hx > 0 ? t : -t;
 }
 
 }  // namespace gm

@@ -56,6 +56,8 @@ int main() {
   exhaustive("sinf", [](float x) { return sinf_(x); }, [](float x) { return ::sinf(x); });
   exhaustive("cosf", [](float x) { return cosf_(x); }, [](float x) { return ::cosf(x); });
   exhaustive("acosf", [](float x) { return acosf_(x); }, [](float x) { return ::acosf(x); });
+  exhaustive("asinf", [](float x) { return asinf_(x); }, [](float x) { return ::asinf(x); });
+  exhaustive("atanf", [](float x) { return atanf_(x); }, [](float x) { return ::atanf(x); });
   std::mt19937_64 g(7);
   std::uniform_real_distribution<float> ux(1e-7f, 4.0f), uy(-8.0f, 8.0f), u01(0.0f, 1.0f);
   unsigned long long n = 0, bad = 0;
@@ -69,5 +71,13 @@ int main() {
     }
   }
   printf("powf: %llu mismatches in %llu sampled pairs\n", bad, n);
+  std::uniform_real_distribution<float> us(-1.0f, 1.0f);
+  bad = 0;
+  for (int i = 0; i < 20000000; ++i) {  // get_sphere_uv's atan2f(p.z, p.x) on unit vectors, and general pairs
+    float y = us(g), x = us(g);
+    if (i & 1) y *= 1000.0f;
+    if (!same(atan2f_(y, x), ::atan2f(y, x))) ++bad;
+  }
+  printf("atan2f: %llu mismatches in 20000000 sampled pairs\n", bad);
   return 0;
 }
