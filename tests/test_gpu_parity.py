@@ -112,6 +112,7 @@ def test_larger_renders_match_oracle_on_sampled_pixels(factory, nx, ny, spp):
     pc = parity.compare_paths(out["paths"][pix], ref["paths"])
     print(pc)
     assert pc["match"] >= parity.MIN_MATCH, pc
+    assert pc["bitexact"] >= parity.MIN_BITEXACT, pc
 
 
 def _nan_panel_scene():
@@ -144,6 +145,7 @@ def test_nan_rays_through_meshes_match_oracle():
     pc = parity.compare_paths(out["paths"], ref["paths"])
     print("nan panel:", pc, out["stats"]["world_rays"], int(ref["stats"][0]))
     assert pc["match"] >= parity.MIN_MATCH, pc
+    assert pc["bitexact"] >= parity.MIN_BITEXACT, pc
     assert abs(out["stats"]["world_rays"] - int(ref["stats"][0])) <= 0.01 * int(ref["stats"][0])
 
 
@@ -186,3 +188,4 @@ def test_model_file_scene_matches_oracle(tmp_path):
     pc = parity.compare_paths(out["paths"], ref["paths"])
     print("model scene:", pc)
     assert pc["match"] >= parity.MIN_MATCH, pc
+    assert pc["bitexact"] >= parity.MIN_BITEXACT, pc

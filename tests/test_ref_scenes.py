@@ -149,5 +149,7 @@ def test_gpu_reference_builders(standin, name):
     out = capi.Renderer(text, device=0).render(nx, ny, spp, 50, keep_paths=True)
     ref = ob.render(text, nx, ny, spp, 50)
     pc = parity.compare_paths(out["paths"], ref["paths"])
+    print(name, pc)
     assert pc["match"] >= parity.MIN_MATCH, (name, pc)
+    assert pc["bitexact"] >= parity.MIN_BITEXACT, (name, pc)
     assert abs(int(out["stats"]["world_rays"]) - int(ref["stats"][0])) <= 0.01 * int(ref["stats"][0])
