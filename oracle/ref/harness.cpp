@@ -11,6 +11,8 @@
 //
 // Commands:
 //   render <scene.txt> <nx> <ny> <ns> <maxdepth> <out_prefix>
+//   sums   <scene.txt> <nx> <ny> <ns> <maxdepth> <pix0> <pix1> <out_prefix>
+//                                                 per-pixel digest (full frames)
 //   bvh    <scene.txt> <obj_id> <out.txt>          reference BVH topology
 //   teapot <scale> <divs> <out.f32>                tessellated vertices
 //   sobol  <N> <out.f64>
@@ -24,6 +26,8 @@
 #undef private
 
 #include "../scene_text.h"
+
+#include <unistd.h>
 
 using srr_text::Cmd;
 
@@ -207,11 +211,15 @@ void reseed_path(unsigned x, unsigned y, unsigned s) {
 double** sobol(unsigned N) {
   // The reference reads its direction numbers from new-joe-kuo-6.21201; for
   // D = 2 only the header line and line 2 ("2 1 0 1") are consumed.
-  const char* path = "/tmp/srr_ref_sobol_dirs.txt";
+  // (per-process file: several harness processes may run at once)
+  char path[64];
+  snprintf(path, sizeof path, "/tmp/srr_ref_sobol_dirs.%d.txt", (int)getpid());
   FILE* f = fopen(path, "w");
   fprintf(f, "d       s       a       m_i\n2       1       0       1\n");
   fclose(f);
-  return sobol_points(N, 2, path);
+  double** sp = sobol_points(N, 2, path);
+  remove(path);
+  return sp;
 }
 
 void write(const std::string& path, const void* p, size_t n) {
@@ -270,6 +278,64 @@ int render_to(hitable* world, hitable* lights, camera* cam, const std::string& o
   for (int p = 0; p < nx * ny; ++p) ppm << img8[p * 3] << " " << img8[p * 3 + 1] << " " << img8[p * 3 + 2] << "\n";
   printf("{\"paths\": %lld, \"world_rays\": %lld, \"ms\": %.3f, \"msamples_per_s\": %.4f}\n",
          (long long)nx * ny * ns, cw.n, ms, cw.n / (ms * 1e3));
+  return 0;
+}
+
+// Per-pixel digest of a render, for frames too large to keep per path (the full
+// 512x512x1024 C2 frame is 268 M paths).  Per pixel, in PPM order:
+//   rays  uint32  sum of the pixel's world->hit calls over its ns paths
+//   hash  uint32  FNV-1a-32 (word-wise: h = (h ^ w) * 16777619) over the words (r, g, b, rays) of each path in
+//                 sample order, every NaN canonicalised to 0x7fc00000 (x86 and
+//                 gfx950 produce different NaN payloads)
+//   mean  3 x f32 the pixel's mean radiance (Raytracing_n.cpp:841-848)
+inline uint32_t fnv_word(uint32_t h, uint32_t w) { return (h ^ w) * 16777619u; }
+inline uint32_t canon_bits(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  return (f != f) ? 0x7fc00000u : u;
+}
+
+// sums <scene.txt> <nx> <ny> <ns> <maxdepth> <pix0> <pix1> <out_prefix>
+int cmd_sums(int argc, char** argv) {
+  if (argc < 10) return 2;
+  RefScene S = build(srr_text::parse(srr_text::read_file(argv[2])));
+  nx = atoi(argv[3]);
+  ny = atoi(argv[4]);
+  ns = atoi(argv[5]);
+  maxDepth = atoi(argv[6]);
+  const int p0 = atoi(argv[7]), p1 = atoi(argv[8]);
+  const std::string out = argv[9];
+  counting_world cw(S.world);
+  double** sp = sobol(ns);
+  std::vector<uint32_t> rays, hash;
+  std::vector<float> mean;
+  for (int pix = p0; pix < p1; ++pix) {
+    int i = pix % nx;
+    int j = ny - 1 - pix / nx;
+    vec3 col(0, 0, 0);
+    uint32_t h = 2166136261u, rs = 0;
+    for (int s = 0; s < ns; ++s) {
+      reseed_path((unsigned)i, (unsigned)j, (unsigned)s);
+      float u = float(sp[s][0] + i) / float(nx);
+      float v = float(sp[s][1] + j) / float(ny);
+      ray r = S.cam->get_ray(u, v);
+      int depth = 0;
+      long long before = cw.n;
+      vec3 c = color(r, &cw, S.lights, &depth);
+      uint32_t nr = (uint32_t)(cw.n - before);
+      h = fnv_word(fnv_word(fnv_word(fnv_word(h, canon_bits(c[0])), canon_bits(c[1])), canon_bits(c[2])), nr);
+      rs += nr;
+      col += de_nan(c);
+    }
+    col /= float(ns);
+    rays.push_back(rs);
+    hash.push_back(h);
+    for (int c = 0; c < 3; ++c) mean.push_back(col[c]);
+  }
+  write(out + ".rays.u32", rays.data(), rays.size() * 4);
+  write(out + ".hash.u32", hash.data(), hash.size() * 4);
+  write(out + ".mean.f32", mean.data(), mean.size() * 4);
+  printf("{\"pixels\": %d, \"world_rays\": %lld}\n", p1 - p0, cw.n);
   return 0;
 }
 
@@ -436,6 +502,7 @@ int main(int argc, char** argv) {
   try {
     std::string c = argv[1];
     if (c == "render") return cmd_render(argc, argv);
+    if (c == "sums") return cmd_sums(argc, argv);
     if (c == "bvh") return cmd_bvh(argc, argv);
     if (c == "teapot") return cmd_teapot(argc, argv);
     if (c == "sobol") return cmd_sobol(argc, argv);

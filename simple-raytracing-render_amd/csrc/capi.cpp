@@ -372,6 +372,7 @@ int srr_accum_set(srr_renderer* r, const float* sums, int64_t npix, int64_t samp
   HIPCHK(hipMemcpy(r->acc, sums, 3 * npix * sizeof(float), hipMemcpyHostToDevice));
   r->acc_npix = npix;
   r->acc_samples = samples;
+  std::fill(r->acc_key, r->acc_key + 5, -1);  // any frame / shard of npix pixels may continue them
   return 0;
 }
 

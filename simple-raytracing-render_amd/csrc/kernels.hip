@@ -222,13 +222,18 @@ struct TraceCtx {
   mutable int mesh_steps = 0;
 };
 
-// Pruning margin: a subtree is skipped only when its box starts beyond
+// Pruning margin: a subtree is skipped only when its box's UNCLIPPED entry
+// (the slab intersection of the whole line, not clipped to tmin) lies beyond
 // best_t * kPruneSlack along the ray.  The reference tests every leaf box the
 // ray segment [tmin, tmax] crosses and keeps the smallest triangle t (a
-// distance) with ties to the later leaf; a skipped box starts (in exact
-// arithmetic) no nearer than any triangle inside it is hit, so it could only
-// hold a hit at t > best_t unless the triangle's float t were more than 6 %
-// short of its box entry -- far beyond the few-ulp error of both computations.
+// distance) with ties to the later leaf -- and triangle::hit ignores tmin
+// (SURVEY Q4), so a leaf box that passes the [tmin, tmax] test can hold a hit
+// at a parameter below tmin, anywhere from the box's own entry on.  A box whose
+// unclipped entry is beyond the bound therefore holds no hit nearer than
+// best_t, unless the triangle's float t were more than 6 % short of its box
+// entry -- far beyond the few-ulp error of both computations.  (Pruning on the
+// tmin-clipped entry, as round 1 did, lost the nearer self-hits of rays leaving
+// the mesh's own surface: 1,115 world rays of the 512x512x1024 C2 frame.)
 constexpr float kPruneSlack = 1.0625f;
 
 // 4-wide traversal of one mesh; same result as mesh_hit (the reference's
@@ -268,11 +273,12 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
     bool hit[4];
 #define SRR_CHILD(c, C)                                                                  \
   {                                                                                      \
-    float lo_ = tmin, hi_ = bound;                                                       \
+    float lo_ = -INFINITY, hi_ = INFINITY;                                               \
     SRR_SLAB_AX(LX.C, HX.C, r.o.x, inv.x) SRR_SLAB_AX(LY.C, HY.C, r.o.y, inv.y)          \
     SRR_SLAB_AX(LZ.C, HZ.C, r.o.z, inv.z)                                                \
     near[c] = lo_;                                                                       \
-    hit[c] = !(hi_ <= lo_);                                                              \
+    const float a_ = lo_ > tmin ? lo_ : tmin, b_ = hi_ < tmax ? hi_ : tmax;              \
+    hit[c] = !(b_ <= a_) && !(PRUNE && lo_ > bound);                                     \
   }
 #define SRR_SLAB_AX(L, H, O, I)                      \
   {                                                  \
@@ -1316,151 +1322,6 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace(SceneView S0, PathState P
   }
 }
 
-// Persistent trace with dynamic ray fetch (scenes without media).  A wave of
-// the per-ray kernel above runs until its longest mesh traversal ends, with the
-// lanes of finished rays idle (~40 % lane utilisation measured); here each lane
-// runs a small state machine -- world objects in list order, then the mesh's
-// node steps, then the hit record -- and lanes whose ray is done fetch the next
-// one from the active list (one wave-aggregated atomic per refill), so the wave
-// keeps its lanes busy until the list is drained.  Same arithmetic, same
-// results as world_hit + world_record.
-constexpr int kMeshSteps = 4;  // node steps per lane between refill checks
-
-template <bool PRUNE>
-__global__ void __launch_bounds__(kTraceBlock) k_trace_pf(SceneView S, PathState P, const int* active,
-                                                          const int* count, int* fetch, int* lists, int list_cap,
-                                                          int* fam_count, int max_depth, unsigned long long* ctr) {
-  const int n = *count;
-  const int n_world = S.n_world;
-  int p = -1;              // path of the lane's ray; -1 idle
-  bool exhausted = false;  // active list drained for this lane
-  Ray r{};
-  int k = 0;               // next world object
-  float closest = FLT_MAX;
-  int wobj = -1, wprim = -1;
-  float wt = 0;
-  // mesh traversal state (threaded BVH2, mesh_hit)
-  bool in_mesh = false;
-  V3 mo{}, md{}, inv{}, dir{};
-  float bound = 0, to_param = 0;
-  int node = 0, end = 0;
-  float4 nlo{}, nhi{};
-  bool found = false;
-  float best_t = 0;
-  int best_i = -1;
-  uint32_t nbox = 0, ntri = 0;
-  for (;;) {
-    // refill idle lanes
-    const bool need = p < 0 && !exhausted;
-    const uint64_t nm = __ballot(need);
-    if (nm) {
-      const int leader = __ffsll((unsigned long long)nm) - 1;
-      int base = 0;
-      if (lane_id() == leader) base = atomicAdd(fetch, __popcll(nm));
-      base = __shfl(base, leader);
-      if (need) {
-        const int idx = base + __popcll(nm & ((1ull << lane_id()) - 1));
-        if (idx < n) {
-          p = active[idx];
-          const float4 ro = ntl(&P.ray_o[p]), rdv = ntl(&P.ray_d[p]);
-          r = Ray{v3(ro.x, ro.y, ro.z), v3(rdv.x, rdv.y, rdv.z), ro.w};
-          k = 0;
-          closest = FLT_MAX;
-          wobj = -1;
-          wprim = -1;
-        } else {
-          exhausted = true;
-        }
-      }
-    }
-    if (__ballot(p >= 0) == 0) break;
-    int fam = -1, fin_p = -1;
-    if (p >= 0) {
-      if (!in_mesh) {
-        // world objects in order (hitable_list::hit) up to the next mesh
-        while (k < n_world) {
-          const DObj ob = S.objs[k];
-          const Ray lr = chain_in(S, ob, r);
-          if (ob.kind == OBJ_MESH) {
-            const DMesh m = S.meshes[ob.idx];
-            mo = lr.o;
-            md = lr.d;
-            inv = v3(1.0f / md.x, 1.0f / md.y, 1.0f / md.z);
-            const float len = length(md);
-            dir = md / len;
-            to_param = kPruneSlack / len;
-            bound = closest;
-            node = m.node_off;
-            end = m.node_off + m.n_nodes;
-            nlo = S.nodes[2 * (node)];
-            nhi = S.nodes[2 * (node) + 1];
-            found = false;
-            best_i = -1;
-            in_mesh = true;
-            break;
-          }
-          ObjHit h;
-          if (basic_hit<TR_BVH2>(S, ob, lr, 0.001f, closest, false, h, TraceCtx{nullptr, nullptr, nullptr})) {
-            closest = h.t;
-            wobj = k;
-            wprim = h.prim;
-            wt = h.t;
-          }
-          ++k;
-        }
-        if (!in_mesh) {  // all objects done: store the winner, bin by material family
-          store_hit(S, P, p, WorldHit{wobj, wprim, wt}, max_depth, fam);
-          fin_p = p;
-          p = -1;
-        }
-      } else {
-        for (int st = 0; st < kMeshSteps; ++st) {
-          ++nbox;
-          const int skip = __float_as_int(nlo.w);
-          const int leaf = __float_as_int(nhi.w);
-          const bool hit = slab(nlo, nhi, mo, inv, 0.001f, bound);
-          if (hit && leaf >= 0) {
-            const int first = leaf >> 1, cnt = (leaf & 1) + 1;
-            ntri += 2;
-            for (int ti = first; ti < first + cnt; ++ti) {
-              const float4* tp = S.tri_pos + kTriStride * (size_t)ti;
-              const float4 a = tp[0], b = tp[1], c = tp[2];
-              float t, u, v;
-              if (tri_hit(v3(a.x, a.y, a.z), v3(b.x, b.y, b.z), v3(c.x, c.y, c.z), true, mo, dir, t, u, v) &&
-                  (!found || wins(t, ti, best_t, best_i))) {
-                found = true;
-                best_t = t;
-                best_i = ti;
-              }
-            }
-            if (PRUNE && found && best_t * to_param < bound) bound = best_t * to_param;
-          }
-          const int next = (hit && leaf < 0) ? node + 1 : skip;
-          if (next >= end) {  // mesh done: it is the list's latest hit if it hit
-            if (found) {
-              closest = best_t;
-              wobj = k;
-              wprim = best_i;
-              wt = best_t;
-            }
-            ++k;
-            in_mesh = false;
-            break;
-          }
-          node = next;
-          nlo = S.nodes[2 * (node)];
-          nhi = S.nodes[2 * (node) + 1];
-        }
-      }
-    }
-    for (int f = 0; f < 4; ++f) append(fam == f, fin_p, lists + f * list_cap, fam_count + f);
-  }
-  if (ctr) {
-    atomicAdd(ctr, (unsigned long long)nbox);
-    atomicAdd(ctr + 1, (unsigned long long)ntri);
-  }
-}
-
 // Hit records of the traced rays (world_record), kept out of the trace kernels
 // so their register budget stays with the traversal.
 __global__ void __launch_bounds__(256) k_record(SceneView S, PathState P, const int* active, const int* count) {
@@ -2226,7 +2087,7 @@ void launch_trace(const SceneView& S, const PathState& P, const int* active, con
   int g = (max_n + 255) / 256;
   // SRR_TRAVERSAL: bvh4prune (default) | bvh4 | bvh2 = one ray per thread over the
   // SAH 4-wide BVH (with / without closest-hit pruning) or the threaded reference
-  // BVH2; pf | pfprune = persistent dynamic-fetch kernel (slower, kept for study);
+  // BVH2;
   // timed = bvh4prune with per-wave timing records (diagnostics)
   static const int tr = [] {
     const char* e = getenv("SRR_TRAVERSAL");
@@ -2234,26 +2095,9 @@ void launch_trace(const SceneView& S, const PathState& P, const int* active, con
     if (e && !strcmp(e, "bvh4")) return (int)dev::TR_BVH4;
     if (e && !strcmp(e, "bvh4prune")) return (int)dev::TR_BVH4_PRUNE;
     if (e && !strcmp(e, "timed")) return (int)dev::TR_BVH4_TIMED;
-    if (e && !strcmp(e, "pf")) return 10;
-    if (e && !strcmp(e, "pfprune")) return 11;
     return (int)dev::TR_BVH4_PRUNE;
   }();
-  static const int pf_blocks = [] {
-    const char* e = getenv("SRR_PF_BLOCKS");
-    return e ? std::max(1, atoi(e)) : 1024;
-  }();
   const int grec = std::min(g, 2048);
-  if (tr >= 10 && !S.has_media) {
-    int gb = std::min(g, pf_blocks);
-    if (tr == 11)
-      hipLaunchKernelGGL((dev::k_trace_pf<true>), dim3(gb), dim3(dev::kTraceBlock), 0, st, S, P, active, count, fetch,
-                         lists, list_cap, fam_count, max_depth, ctr);
-    else
-      hipLaunchKernelGGL((dev::k_trace_pf<false>), dim3(gb), dim3(dev::kTraceBlock), 0, st, S, P, active, count,
-                         fetch, lists, list_cap, fam_count, max_depth, ctr);
-    hipLaunchKernelGGL(dev::k_record, dim3(grec), dim3(256), 0, st, S, P, active, count);
-    return;
-  }
   static unsigned long long* timing = nullptr;
   if (tr == dev::TR_BVH4_TIMED && !timing) {
     (void)hipMalloc((void**)&timing, (1 + 8 * dev::kTimingCap) * sizeof(unsigned long long));
@@ -2273,7 +2117,7 @@ void launch_trace(const SceneView& S, const PathState& P, const int* active, con
   else if (trm == dev::TR_BVH4) { SRR_LAUNCH_TRACE_W(M, dev::TR_BVH4) }       \
   else if (trm == dev::TR_BVH4_TIMED) { SRR_LAUNCH_TRACE_W(M, dev::TR_BVH4_TIMED) } \
   else { SRR_LAUNCH_TRACE_W(M, dev::TR_BVH4_PRUNE) }
-  const int trm = tr >= 10 ? (int)dev::TR_BVH4_PRUNE : tr;  // media scenes: one ray per thread
+  const int trm = tr;
   if (S.has_media) {
     SRR_LAUNCH_TRACE_M(true)
   } else {

@@ -187,19 +187,51 @@ static int ensure_lane(Lane& L, size_t n, int depth, bool keep, std::string& err
 // Per-pixel running sums: zeroed by a render without SRR_FLAG_CONTINUE; a render
 // with it adds its samples to them, so consecutive sample ranges accumulate in
 // sample order -- bitwise the sums of one render of all of them.
+static void accum_key(const srr_params* p, int key[5]) {
+  const bool whole = p->shard_count <= 1;
+  key[0] = p->nx;
+  key[1] = p->ny;
+  key[2] = whole ? 0 : p->shard_index;
+  key[3] = whole ? 1 : p->shard_count;
+  key[4] = whole ? 0 : p->tile;
+}
+
 static int begin_accum(srr_renderer* r, const srr_params* p, int64_t npix, hipStream_t st, std::string& err) {
+  int key[5];
+  accum_key(p, key);
   if (p->flags & SRR_FLAG_CONTINUE) {
     if (r->acc_npix != npix) {
       err = "SRR_FLAG_CONTINUE: no running sums for this shard (render without the flag or srr_accum_set first)";
       return SRR_EINVAL;
     }
+    if (p->sample_begin != r->acc_samples) {
+      err = "SRR_FLAG_CONTINUE: sample_begin " + std::to_string(p->sample_begin) + " != the " +
+            std::to_string(r->acc_samples) + " samples already in the running sums";
+      return SRR_EINVAL;
+    }
+    if (r->acc_key[0] >= 0 && !std::equal(key, key + 5, r->acc_key)) {
+      err = "SRR_FLAG_CONTINUE: the running sums belong to another frame or shard";
+      return SRR_EINVAL;
+    }
+    std::copy(key, key + 5, r->acc_key);
     return 0;
   }
   RCHK(hipMemsetAsync(r->acc, 0, 3 * npix * sizeof(float), st));
   r->acc_npix = npix;
   r->acc_samples = 0;
+  std::copy(key, key + 5, r->acc_key);
   return 0;
 }
+
+// Invalidates the running sums unless the render that began them committed:
+// a failed render leaves partial sums that no SRR_FLAG_CONTINUE may build on.
+struct AccCommit {
+  srr_renderer* r;
+  bool ok = false;
+  ~AccCommit() {
+    if (!ok) r->acc_npix = 0;
+  }
+};
 
 // Path-resident engine (kernels.hip k_paths): one persistent kernel per window
 // of samples; samples land in a [pixel][sample] buffer that k_accumulate_window
@@ -280,6 +312,7 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
     const int rc = begin_accum(r, p, npix, st, err);
     if (rc < 0) return rc;
   }
+  AccCommit commit{r};
   const bool all_fam = !r->diffuse_only;
   RCHK(hipEventRecord(r->ev_beg, st));
   double kernel_ms = 0;
@@ -317,8 +350,8 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
     kernel_ms += ms;
     s.trace_launches += 1;
   }
-  r->acc_samples += p->spp;
-  launch_finish(r->acc, d_mean, npix, (int)r->acc_samples, st);
+  const int64_t acc_total = r->acc_samples + p->spp;
+  launch_finish(r->acc, d_mean, npix, (int)acc_total, st);
   RCHK(hipEventRecord(r->ev_end, st));
   RCHK(hipStreamSynchronize(st));
   RCHK(hipGetLastError());
@@ -334,6 +367,8 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
     err = "k_paths index guard tripped (bits " + std::to_string(ctr[2]) + ")";
     return SRR_EIO;
   }
+  r->acc_samples = acc_total;
+  commit.ok = true;
   float total = 0;
   RCHK(hipEventElapsedTime(&total, r->ev_beg, r->ev_end));
   s.world_rays = (int64_t)rays;
@@ -352,11 +387,13 @@ int render_device(srr_renderer* r, const srr_params* p, const int32_t* pix, int6
     return e && !strcmp(e, "wave");
   }();
   const bool wave_engine = wave_env || (p->flags & SRR_FLAG_WAVEFRONT);
+  // every buffer either engine allocates belongs to the renderer's device,
+  // whatever device the caller has current
+  RCHK(hipSetDevice(r->device));
   // the path engine stages the world tables in LDS when they fit
   // (kernels.hip kWorldLdsBytes) and reads them from global memory otherwise
   if (!wave_engine && !(p->flags & SRR_FLAG_COUNT_VISITS))
     return render_paths(r, p, pix, npix, d_mean, stats, err);
-  RCHK(hipSetDevice(r->device));
   const bool keep = (p->flags & SRR_FLAG_KEEP_PATHS) != 0;
   const int R = kRegionsPerLane;
   hipStream_t ast = r->acc_st;
@@ -442,6 +479,7 @@ int render_device(srr_renderer* r, const srr_params* p, const int32_t* pix, int6
     const int rc = begin_accum(r, p, npix, ast, err);
     if (rc < 0) return rc;
   }
+  AccCommit commit{r};
   RCHK(hipEventRecord(r->ev_beg, ast));
   for (int l = 0; l < lanes; ++l) {
     Lane& L = r->lanes[l];
@@ -562,11 +600,13 @@ int render_device(srr_renderer* r, const srr_params* p, const int32_t* pix, int6
     }
     if (!progress) std::this_thread::yield();
   }
-  r->acc_samples += p->spp;
-  launch_finish(r->acc, d_mean, npix, (int)r->acc_samples, ast);
+  const int64_t acc_total = r->acc_samples + p->spp;
+  launch_finish(r->acc, d_mean, npix, (int)acc_total, ast);
   RCHK(hipEventRecord(r->ev_end, ast));
   RCHK(hipStreamSynchronize(ast));
   RCHK(hipGetLastError());
+  r->acc_samples = acc_total;
+  commit.ok = true;
   float total = 0;
   RCHK(hipEventElapsedTime(&total, r->ev_beg, r->ev_end));
   s.total_ms = total;

@@ -60,6 +60,9 @@ struct srr_renderer {
   float* acc = nullptr;
   int64_t acc_npix = 0;     // pixels the running sums cover (SRR_FLAG_CONTINUE)
   int64_t acc_samples = 0;  // samples per pixel accumulated in them
+  // the frame and shard the running sums belong to: {nx, ny, shard_index,
+  // shard_count, tile}; all -1 after srr_accum_set (only npix is known then)
+  int acc_key[5] = {-1, -1, -1, -1, -1};
   unsigned long long* visits = nullptr;  // SRR_FLAG_COUNT_VISITS counters (3)
   // path-resident engine (render_paths)
   int pw_lanes = 0;

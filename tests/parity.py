@@ -3,7 +3,8 @@
 Tolerance (written here and in DESIGN.md §6): a path matches when
 its radiance equals the reference's within 1e-3 relative (|a-b| <= 1e-3 *
 max(|a|, |b|) + 1e-6 per channel), NaN matching NaN; >= 99 % of paths must
-match; bit-identical paths are reported separately."""
+match (the tolerance SURVEY §8(d) proposes), and -- the bar the GPU tests actually
+hold -- every path must be bit-identical (MIN_BITEXACT = 1.0)."""
 from __future__ import annotations
 
 import numpy as np
@@ -11,7 +12,7 @@ import numpy as np
 REL_TOL = 1e-3
 ABS_TOL = 1e-6
 MIN_MATCH = 0.99
-MIN_BITEXACT = 0.999  # golden renders: measured 1.0 on the MI355X
+MIN_BITEXACT = 1.0  # every path bit-identical (NaN payloads aside): DESIGN.md §2
 
 
 def compare_paths(got: np.ndarray, want: np.ndarray) -> dict:

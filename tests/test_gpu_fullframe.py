@@ -1,0 +1,47 @@
+"""GPU parity on the FULL headline frame: C2 (Cornell box + 6,400-tri teapot,
+512x512x1024, maxDepth 50) rendered by the HIP path through the C-ABI, every
+one of its 268 M paths checked bit for bit against the reference's own render
+of the same frame via per-pixel digests (tests/golden/c2_full.npz, made by
+oracle/_ref/ref_harness; tests/fullframe.py).  Exact equality: world-ray sums,
+per-path radiance bits (NaN payloads aside) and the mean image.
+
+On a mismatch, with SRR_DIAG_DIR set, the failing pixels' per-path outputs are
+saved there for bisection against the CPU restatement (tools/diag_fullframe.py)."""
+import os
+
+import numpy as np
+import pytest
+
+import fullframe
+from srr import capi
+
+pytestmark = pytest.mark.gpu
+
+
+def _save_diag(name, bad, out):
+    d = os.environ.get("SRR_DIAG_DIR")
+    if not d or bad.size == 0:
+        return
+    os.makedirs(d, exist_ok=True)
+    bad = bad[:4096]
+    np.savez_compressed(os.path.join(d, f"{name}_diff.npz"), pixels=bad, paths=out["paths"][bad],
+                        rays=out["rays"][bad], mean=out["mean"][bad])
+
+
+@pytest.mark.parametrize("engine", ["paths"])
+def test_c2_full_frame_is_the_reference_frame(engine):
+    name = "c2_full"
+    m = fullframe.meta(name)
+    want = fullframe.load(name)
+    r = capi.Renderer(fullframe.scene_text(name))
+    out = r.render(m["nx"], m["ny"], m["spp"], m["max_depth"], keep_paths=True)
+    got = fullframe.digest(out["paths"], out["rays"])
+    got["mean"] = out["mean"]
+    res = fullframe.compare(got, want)
+    res["stats_world_rays"] = out["stats"]["world_rays"]
+    print(name, res)
+    bad = np.flatnonzero((got["hash"] != want["hash"]) | (got["rays"] != want["rays"]))
+    _save_diag(name, bad, out)
+    assert out["stats"]["world_rays"] == m["world_rays"], res
+    assert res["ray_mismatch_pixels"] == 0 and res["hash_mismatch_pixels"] == 0, res
+    assert res["mean_mismatch_pixels"] == 0, res

@@ -67,3 +67,21 @@ def test_continue_without_state_is_an_error():
     r = capi.Renderer(sc.text())
     with pytest.raises(capi.SrrError):
         r.render(8, 8, 2, 50, flags=capi.FLAG_CONTINUE, sample_begin=2)
+
+
+@pytest.mark.gpu
+def test_continue_rejects_a_mismatched_resume():
+    """The running sums know their sample count and their frame / shard: a
+    resume at the wrong sample or with another shard is an error, and the sums
+    survive it intact."""
+    sc, _ = scenes.s1_cornell()
+    r = capi.Renderer(sc.text())
+    nx, ny = 32, 32
+    r.render(nx, ny, 3, 50, shard=(0, 2), tile=16)
+    with pytest.raises(capi.SrrError):  # 3 samples are in the sums, not 2
+        r.render(nx, ny, 2, 50, shard=(0, 2), tile=16, flags=capi.FLAG_CONTINUE, sample_begin=2)
+    with pytest.raises(capi.SrrError):  # same pixel count, other shard
+        r.render(nx, ny, 2, 50, shard=(1, 2), tile=16, flags=capi.FLAG_CONTINUE, sample_begin=3)
+    got = r.render(nx, ny, 2, 50, shard=(0, 2), tile=16, flags=capi.FLAG_CONTINUE, sample_begin=3)["mean"]
+    want = capi.Renderer(sc.text()).render(nx, ny, 5, 50, shard=(0, 2), tile=16)["mean"]
+    np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))

@@ -152,4 +152,4 @@ def test_gpu_reference_builders(standin, name):
     print(name, pc)
     assert pc["match"] >= parity.MIN_MATCH, (name, pc)
     assert pc["bitexact"] >= parity.MIN_BITEXACT, (name, pc)
-    assert abs(int(out["stats"]["world_rays"]) - int(ref["stats"][0])) <= 0.01 * int(ref["stats"][0])
+    assert int(out["stats"]["world_rays"]) == int(ref["stats"][0])
