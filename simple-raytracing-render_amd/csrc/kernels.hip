@@ -526,20 +526,38 @@ SRR_D bool basic_hit(const SceneView& S, const DObj& ob, const Ray& lr, float tm
   }
 }
 
-// hitable_list::hit (hitable_list.h:21-33) over objects [b, b+n) -- used for a
-// medium's boundary (which sees is_medium = true)
+// hitable_list::hit (hitable_list.h:21-33) over objects [b, b+n) -- a medium's
+// boundary, which sees is_medium = true
 template <int TR>
-SRR_D bool list_hit(const SceneView& S, int b, int n, const Ray& r, float tmin, float tmax, bool is_medium, float& t,
+SRR_D bool list_hit(const SceneView& S, int b, int n, const Ray& r, float tmin, float tmax, float& t,
                     const TraceCtx& cx) {
   bool any = false;
   float closest = tmax;
   for (int k = 0; k < n; ++k) {
     const DObj ob = wload<TR>(S.objs, b + k);
-    ObjHit h;
-    if (basic_hit<TR>(S, ob, chain_in<TR>(S, ob, r), tmin, closest, is_medium, h, cx)) {
+    const Ray lr = chain_in<TR>(S, ob, r);
+    float th = 0;
+    bool hit;
+    if (ob.kind == OBJ_MESH) {
+      // a mesh inside a boundary (rare: the shipped scenes bound their media with
+      // spheres and boxes) takes the exact stackless BVH2 walk, so the medium path
+      // does not inline two more copies of the LDS-stack BVH4 traversal into the
+      // path kernel (that pushed the MEDIA variants to ~110 spilled VGPRs)
+      MeshHit mh;
+      hit = mesh_hit<false>(S, wload<TR>(S.meshes, ob.idx), lr, tmin, closest, true, mh, nullptr);
+      th = mh.t;
+    } else if (ob.kind == OBJ_OBVH) {
+      int po;
+      hit = obvh_hit<TR>(S, S.obvhs[ob.idx], lr, tmin, closest, true, th, po);
+    } else if (ob.kind == OBJ_MEDIUM) {
+      hit = false;
+    } else {
+      hit = prim_hit<TR>(S, ob, lr, tmin, closest, true, th);
+    }
+    if (hit) {
       any = true;
-      closest = h.t;
-      t = h.t;
+      closest = th;
+      t = th;
     }
   }
   return any;
@@ -550,21 +568,28 @@ template <int TR>
 SRR_D bool medium_hit(const SceneView& S, const DMedium& md, const Ray& r, float tmin, float tmax, Rng& rng,
                       float& t, const TraceCtx& cx) {
   (void)(drand(rng) < 0.00001);
-  float t1, t2;
-  if (list_hit<TR>(S, md.bnd_begin, md.bnd_count, r, -FLT_MAX, FLT_MAX, true, t1, cx)) {
-    if (list_hit<TR>(S, md.bnd_begin, md.bnd_count, r, t1 + 0.0001, FLT_MAX, true, t2, cx)) {
-      if (t1 < tmin) t1 = tmin;
-      if (t2 > tmax) t2 = tmax;
-      if (t1 >= t2) return false;
-      if (t1 < 0) t1 = 0;
-      float len = length(r.d);
-      float inside = (t2 - t1) * len;
-      float hit_distance = -(1 / md.density) * ::log(drand(rng));
-      if (hit_distance < inside) {
-        t = t1 + hit_distance / len;
-        return true;
-      }
-    }
+  // the boundary's entry (from -FLT_MAX) and exit (from entry + 0.0001, a double
+  // sum rounded to the float parameter): one inlined list walk, run twice
+  float tb[2] = {0, 0};
+  float lo = -FLT_MAX;
+#pragma unroll 1
+  for (int pass = 0; pass < 2; ++pass) {
+    float th;
+    if (!list_hit<TR>(S, md.bnd_begin, md.bnd_count, r, lo, FLT_MAX, th, cx)) return false;
+    tb[pass] = th;
+    lo = (float)((double)th + 0.0001);
+  }
+  float t1 = tb[0], t2 = tb[1];
+  if (t1 < tmin) t1 = tmin;
+  if (t2 > tmax) t2 = tmax;
+  if (t1 >= t2) return false;
+  if (t1 < 0) t1 = 0;
+  float len = length(r.d);
+  float inside = (t2 - t1) * len;
+  float hit_distance = -(1 / md.density) * ::log(drand(rng));
+  if (hit_distance < inside) {
+    t = t1 + hit_distance / len;
+    return true;
   }
   return false;
 }
