@@ -1113,6 +1113,7 @@ struct Bsdf {
   // bounce (bsdf_prepare) instead of once per resampling iteration
   float co;        // cosine_pdf: dot(unit_vector(wo), n)
   V3 lo;           // onrennayar_pdf: local unit(-wo)
+  bool flip;       // cosine_pdf / onrennayar_pdf generate: dot(-wo, n) > 0
 };
 
 SRR_D V3 to_local_unit(const Onb& b, V3 d) {
@@ -1137,13 +1138,14 @@ SRR_D V3 bsdf_generate(Bsdf& f, V3 wo, Rng& rng) {
   }
   // cosine_pdf / onrennayar_pdf (pdf.h:47-56, 103-112)
   V3 g = random_cosine_direction(rng);
-  if (dot(-wo, f.n) > 0) g.z *= -1;
+  if (f.flip) g.z *= -1;  // dot(-wo, n) > 0, computed by bsdf_prepare
   return onb_local(f.uvw, g);
 }
 
 template <bool BECK>
 SRR_D void bsdf_prepare(Bsdf& f, V3 wo) {
   if (BECK) return;
+  f.flip = dot(-wo, f.n) > 0;
   if (f.kind == MAT_LAMBERTIAN) f.co = dot(unit_vector(wo), f.n);
   else f.lo = to_local_unit(f.uvw, -wo);
 }
@@ -1225,6 +1227,170 @@ __device__ __forceinline__ void append4(int fam, int value, int* lists, int list
   if (fam >= 0) {
     const uint64_t m = fam == 0 ? m0 : fam == 1 ? m1 : fam == 2 ? m2 : m3;
     lists[fam * list_cap + base + __popcll(m & ((1ull << l) - 1))] = value;
+  }
+}
+
+// ---------------------------------------------- wave-cooperative mixture loop
+// The resampling loop of a diffuse bounce (Raytracing_n.cpp:75-89: draw from the
+// 50/50 light / BSDF mixture until its pdf is non-zero) needs ~2
+// attempts per lane but a wave would run until its slowest lane is done (~7 for
+// 64 lanes).  Instead the wave runs the loops of all its pending lanes together:
+// per round every lane evaluates one attempt of some pending path, the k-th
+// helper of a path taking attempt tries+k.  That attempt's LCG state is the
+// path's state advanced over k attempts' draws, and an attempt's draw count is a
+// function of the state alone (branch draw; light: index draw + 2 if the light
+// samples, BSDF: 2), so skip_attempt() reaches it exactly.  Each path keeps its
+// first successful attempt (direction, pdf, LCG state after it): bit for bit the
+// sequential loop's result.  Only the LCG is drawn in a diffuse mixture loop.
+
+// what one attempt of a path's mixture loop reads (plus its LCG state)
+struct DiffSetup {
+  V3 p;          // hit point (light sampling origin)
+  V3 w, v;       // the bounce's onb (u = cross(w, v), exactly as onb_from_w)
+  V3 nl;         // lambertian: n (bsdf value); orennayar: local unit(-wo)
+  float c0, c1;  // lambertian: co; orennayar: A, B
+  int flags;     // bit 0: orennayar, bit 1: flip (dot(-wo, n) > 0)
+};
+
+SRR_D DiffSetup diff_setup(const Bsdf& f, V3 p) {
+  const bool on = f.kind != MAT_LAMBERTIAN;
+  return DiffSetup{p, f.uvw.w, f.uvw.v, on ? f.lo : f.n, on ? f.A : f.co, f.B, (on ? 1 : 0) | (f.flip ? 2 : 0)};
+}
+
+SRR_D Bsdf bsdf_of(const DiffSetup& d) {
+  Bsdf f;
+  f.kind = (d.flags & 1) ? (int)MAT_ORENNAYAR : (int)MAT_LAMBERTIAN;
+  f.uvw.w = d.w;
+  f.uvw.v = d.v;
+  f.uvw.u = cross(d.w, d.v);
+  f.n = d.nl;
+  f.lo = d.nl;
+  f.co = d.c0;
+  f.A = d.c0;
+  f.B = d.c1;
+  f.flip = (d.flags & 2) != 0;
+  return f;
+}
+
+// one attempt of the loop body (Raytracing_n.cpp:76-88; pdf.h:183-192)
+SRR_D float mixture_attempt(const SceneView& S, Bsdf& f, V3 hpt, Rng& rng, V3& ndir) {
+  if (drand(rng) < 0.5) ndir = lights_random(S, hpt, rng);
+  else ndir = bsdf_generate<false>(f, v3(0.f), rng);
+  return 0.5 * lights_pdf(S, hpt, ndir) + 0.5 * bsdf_value<false>(f, v3(0.f), ndir);
+}
+
+SRR_D uint64_t lcg_step(uint64_t s) { return (0x5DEECE66DULL * s + 0xB16ULL) & 0xFFFFFFFFFFFFULL; }
+
+// the LCG state after one attempt's draws, from the state before it
+SRR_D uint64_t skip_attempt(const SceneView& S, uint64_t s) {
+  s = lcg_step(s);                      // drand() < 0.5: the branch
+  if ((s >> 47) == 0) {                 // light: hitable_list::random (hitable_list.h:63-67)
+    s = lcg_step(s);                    // the light index
+    const int idx = int((double)(uint32_t)(s >> 16) / 4294967296.0 * S.n_lights);
+    if (S.lights[idx].kind != LIGHT_NONE) s = lcg_step(lcg_step(s));  // xz_rect / sphere / triangle: 2
+  } else {
+    s = lcg_step(lcg_step(s));          // random_cosine_direction: 2
+  }
+  return s;
+}
+
+constexpr int kMixtureGuard = 100000;  // the sequential loop's attempt cap (scatter)
+#ifndef SRR_COOP_HELPERS
+#define SRR_COOP_HELPERS 8
+#endif
+#ifndef SRR_COOP_ID0
+#define SRR_COOP_ID0 0
+#endif
+constexpr int kMaxHelpers = SRR_COOP_HELPERS;  // attempts of one path per round
+
+// Runs to completion the loops of every lane with `pend` (converged wave, all 64
+// lanes active).  In: the lane's setup, its LCG state before attempt `tries`.
+// Out: ndir, pdf and the LCG state after the first attempt with pdf != 0 (or the
+// guard's last attempt).  The first round is each pending lane's own attempt
+// (no exchange); later rounds spread the remaining paths over all 64 lanes.
+SRR_D void coop_mixture(const SceneView& S, const DiffSetup& me, bool& pend, int& tries, uint64_t& lcg, V3& ndir,
+                        float& pdf) {
+  const int lane = lane_id();
+  const uint64_t lt = (1ull << lane) - 1;
+  uint64_t F = __ballot(pend);
+  bool first = SRR_COOP_ID0 != 0;
+  while (F) {
+    const int nF = __popcll(F);
+    const int rank = pend ? __popcll(F & lt) : nF + __popcll(~F & lt);
+    DiffSetup d;
+    int t0, k;
+    uint64_t s;
+    if (first) {
+      d = me;
+      t0 = tries;
+      s = lcg;
+      k = pend ? 0 : kMaxHelpers;
+    } else {
+      // lane r < nF learns the lane of the r-th pending path (a permutation of
+      // all 64 lanes: pending lanes in order, then the others)
+      const int owner_of = __builtin_amdgcn_ds_permute(rank << 2, lane);
+      const int q = lane % nF;
+      k = lane / nF;
+      const int src = __builtin_amdgcn_ds_bpermute(q << 2, owner_of);
+      d.p = v3(__shfl(me.p.x, src), __shfl(me.p.y, src), __shfl(me.p.z, src));
+      d.w = v3(__shfl(me.w.x, src), __shfl(me.w.y, src), __shfl(me.w.z, src));
+      d.v = v3(__shfl(me.v.x, src), __shfl(me.v.y, src), __shfl(me.v.z, src));
+      d.nl = v3(__shfl(me.nl.x, src), __shfl(me.nl.y, src), __shfl(me.nl.z, src));
+      d.c0 = __shfl(me.c0, src);
+      d.c1 = __shfl(me.c1, src);
+      d.flags = __shfl(me.flags, src);
+      t0 = __shfl(tries, src);
+      s = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(lcg >> 32), src) << 32) |
+          (uint32_t)__shfl((int)(uint32_t)lcg, src);
+    }
+    const bool active = k < kMaxHelpers && t0 + k < kMixtureGuard;
+    V3 nd = v3(0.f);
+    float pv = 0;
+    if (active) {
+      for (int j = 0; j < k; ++j) s = skip_attempt(S, s);
+      Rng rr{s, 0};
+      Bsdf f = bsdf_of(d);
+      pv = mixture_attempt(S, f, d.p, rr, nd);
+      s = rr.lcg;
+    }
+    const uint64_t ok = __ballot(active && (pv != 0 || t0 + k + 1 >= kMixtureGuard));
+    if (first) {  // every pending lane ran its own next attempt
+      if (pend) {
+        lcg = s;
+        if ((ok >> lane) & 1) {
+          ndir = nd;
+          pdf = pv;
+          pend = false;
+        } else {
+          tries += 1;
+        }
+      }
+      first = false;
+    } else {
+      // owner: its first successful helper (k ascending), else its last one
+      int win = lane, m = 0;
+      if (pend) {
+        m = min(kMaxHelpers, (63 - rank) / nF + 1);
+        m = min(m, kMixtureGuard - tries);
+        int j = 0;
+        while (j < m - 1 && !((ok >> (rank + j * nF)) & 1)) ++j;
+        win = rank + j * nF;
+      }
+      const float wx = __shfl(nd.x, win), wy = __shfl(nd.y, win), wz = __shfl(nd.z, win), wp = __shfl(pv, win);
+      const uint64_t ws = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(s >> 32), win) << 32) |
+                          (uint32_t)__shfl((int)(uint32_t)s, win);
+      if (pend) {
+        lcg = ws;
+        if ((ok >> win) & 1) {
+          ndir = v3(wx, wy, wz);
+          pdf = wp;
+          pend = false;
+        } else {
+          tries += m;
+        }
+      }
+    }
+    F = __ballot(pend);
   }
 }
 
@@ -1696,6 +1862,15 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
       cx.mesh_cycles = 0;
       ++it;
     }
+    bool done = false;
+    V3 C = v3(0.f);
+    // a diffuse bounce with lights: set up here, its mixture loop runs below with
+    // the whole wave (coop_mixture), then its record is written
+    bool diff = false, pend = false;
+    DiffSetup ds{};
+    V3 d_atten = v3(0.f), d_n = v3(0.f), d_dir = v3(0.f);
+    float d_pdf = 0;
+    int d_tries = 0;
     if (g >= 0) {
       ++prays;
       const WorldHit w = world_hit<MEDIA, TIMED ? (TR_BVH4_TIMED | (WL ? TR_WL : 0)) : TR>(S, r, rng, cx);
@@ -1705,8 +1880,7 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
         tp[2] += cx.mesh_cycles;
         tq = t;
       }
-      bool done = true;
-      V3 C = v3(0.f);
+      done = true;
       if (w.obj >= 0) {
         const HitRec h = world_record<TR>(S, r, w);
         const int kind = h.mat >= 0 ? S.mats[h.mat].kind : -1;
@@ -1719,6 +1893,22 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
         const int fam = family_of(h.mat, kind, depth, W.max_depth);
         if (fam == FAM_TERM) {
           C = hit_emitted(S, h.mat, r.d, h.p, h.n, h.u, h.v);
+        } else if ((!ALLFAM || fam == FAM_DIFF) && S.n_lights > 0) {
+          // scatter<FAM_DIFF> up to its resampling loop (Raytracing_n.cpp:73-75)
+          const DMat M = S.mats[h.mat];
+          d_atten = tex_value(S, M.tex, h.u, h.v, h.p);
+          Bsdf f;
+          f.kind = M.kind;
+          f.n = h.n;
+          f.uvw = onb_from_w(h.n);
+          f.A = M.p[0];
+          f.B = M.p[1];
+          bsdf_prepare<false>(f, r.d);
+          ds = diff_setup(f, h.p);
+          (void)drand(rng);  // mixture_pdf ctor (pdf.h:175)
+          d_n = h.n;
+          diff = pend = true;
+          done = false;
         } else {
           const DMat M = S.mats[h.mat];
           float4 rec;
@@ -1736,6 +1926,18 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
           done = false;
         }
       }
+    }
+    if (__ballot(pend)) coop_mixture(S, ds, pend, d_tries, rng.lcg, d_dir, d_pdf);
+    if (diff) {  // the rest of scatter<FAM_DIFF>: scattering_pdf and the record
+      float c = dot(d_n, unit_vector(d_dir));  // material.h:100-105, 134-138
+      if (c < 0) c = 0;
+      const V3 as = d_atten * (c / kPi);
+      if (depth >= W.max_depth || slot >= W.lanes) atomicOr(W.err, 2);
+      else nts(&W.rec[(size_t)depth * W.lanes + slot], make_float4(as.x, as.y, as.z, d_pdf));
+      r = Ray{ds.p, d_dir, r.tm};
+      ++depth;
+    }
+    if (g >= 0) {
       if (TIMED) {
         const uint64_t t = __builtin_amdgcn_s_memtime();
         tp[3] += t - tq;
