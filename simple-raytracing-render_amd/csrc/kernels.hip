@@ -1622,10 +1622,15 @@ SRR_D V3 hit_emitted(const SceneView& S, int mat, V3 rdir, V3 hpt, V3 nrm, float
   return v3(0.f);
 }
 
+// The pdf slot of a specular bounce's record: a signalling NaN, which no float
+// arithmetic or conversion produces (their NaNs are quiet), so the path kernel's
+// fold tells specular records from any diffuse pdf without a per-path bit mask.
+constexpr uint32_t kSpecMark = 0x7f800001u;
+
 // The scattering half of one color() bounce for family F (Raytracing_n.cpp:63-94,
 // material.h): the next direction and time, and the bounce's record for the
 // back-to-front fold: (attenuation * scattering_pdf, pdf) or, specular,
-// (attenuation, 0) with `spec` set.
+// (attenuation, kSpecMark) with `spec` set.
 template <int F>
 SRR_D void scatter(const SceneView& S, const DMat& M, V3 rdir, float rtime, V3 hpt, V3 nrm, float hu, float hv,
                    Rng& rng, float4& rec, bool& spec, V3& ndir, float& ntime) {
@@ -1671,7 +1676,7 @@ SRR_D void scatter(const SceneView& S, const DMat& M, V3 rdir, float rtime, V3 h
       ndir = random_in_unit_sphere(rng);
       atten = tex_value(S, M.tex, hu, hv, hpt);
     }
-    rec = make_float4(atten.x, atten.y, atten.z, 0.f);
+    rec = make_float4(atten.x, atten.y, atten.z, __uint_as_float(kSpecMark));
     spec = true;
   } else {
     // lambertian / orennayar / beckmann: mixture(light, bsdf) (Raytracing_n.cpp:73-94)
@@ -1754,6 +1759,17 @@ SRR_D bool shade_one(const SceneView& S, const PathState& P, int p, int max_dept
 // recursion returns, writes the sample and fetches the next (pixel, sample) from
 // a global cursor (one wave-aggregated atomic per refill).  No path state goes
 // through memory between bounces except the write-only bounce records.
+// bounce records: plain stores keep the first bounces' records (a few MB per
+// XCD) in L2 for the fold; nontemporal ones stream them to HBM
+#ifndef SRR_REC_NT
+#define SRR_REC_NT 0
+#endif
+SRR_D void rec_store(float4* p, float4 v) {
+  if (SRR_REC_NT) nts(p, v);
+  else *p = v;
+}
+SRR_D float4 rec_load(const float4* p) { return SRR_REC_NT ? ntl(p) : *p; }
+
 constexpr int kPathsBlock = 256;
 constexpr unsigned long long kPoolChunk = 64;  // path indices a wave takes per cursor atomic
 
@@ -1791,66 +1807,61 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
   cx.lds_nodes = (const __attribute__((address_space(3))) f32x4*)s_n4;
   cx.lds_count = S0.node4_lds;
   const int slot = blockIdx.x * blockDim.x + threadIdx.x;
-  long long g = -1;  // path of this lane, -1 idle
-  bool exhausted = false;
-  unsigned long long pool = 0, pool_end = 0;  // the wave's unissued path indices [pool, pool_end)
-  unsigned long long nxt_lane0 = 0;           // lane 0: base of the armed next chunk
+  int g = -1;  // path of this lane (a window numbers its paths below 2^31), -1 idle
+  const uint32_t n_paths = (uint32_t)W.n_paths;
+  // the wave's unissued path indices [pool, pool_end): wave-uniform (scalar)
+  uint32_t pool = 0, pool_end = 0;
+  uint32_t nxt_lane0 = 0;  // lane 0: base of the armed next chunk
   bool nxt_armed = false;
   Ray r{};
   Rng rng{};
   int depth = 0;
-  uint64_t spec = 0;
-  uint32_t prays = 0, nrays = 0;
+  uint32_t nrays = 0;
   for (;;) {
     uint64_t tq = TIMED ? __builtin_amdgcn_s_memtime() : 0;
     // refill lanes whose path ended, from the wave's pool of path indices; the
     // pool is re-armed one chunk ahead (an atomic whose result is first read an
     // iteration later, so its latency hides behind that iteration's work)
-    const bool need = g < 0 && !exhausted;
+    const bool need = g < 0;
     const uint64_t nm = __ballot(need);
-    if (nm) {
-      const unsigned long long cnt = __popcll(nm);
-      const unsigned long long rank = __popcll(nm & ((1ull << lane_id()) - 1));
-      unsigned long long avail = pool_end - pool;
-      long long idx;
+    if (nm && pool < n_paths) {
+      const uint32_t cnt = __popcll(nm);
+      const uint32_t rank = __popcll(nm & ((1ull << lane_id()) - 1));
+      const uint32_t avail = pool_end - pool;
+      uint32_t idx;
       if (avail >= cnt) {
-        idx = (long long)(pool + rank);
+        idx = pool + rank;
         pool += cnt;
       } else {
-        unsigned long long nb;
+        uint32_t nb;
         if (nxt_armed) {
-          nb = __shfl(nxt_lane0, 0);
+          nb = __builtin_amdgcn_readfirstlane(nxt_lane0);
           nxt_armed = false;
         } else {
-          unsigned long long b = 0;
-          if (lane_id() == 0) b = atomicAdd(W.cursor, (unsigned long long)kPoolChunk);
-          nb = __shfl(b, 0);
+          uint32_t b = 0;
+          if (lane_id() == 0) b = (uint32_t)atomicAdd(W.cursor, (unsigned long long)kPoolChunk);
+          nb = __builtin_amdgcn_readfirstlane(b);
         }
-        idx = (long long)(rank < avail ? pool + rank : nb + (rank - avail));
+        idx = rank < avail ? pool + rank : nb + (rank - avail);
         pool = nb + (cnt - avail);
-        pool_end = nb + kPoolChunk;
+        pool_end = nb + (uint32_t)kPoolChunk;
       }
-      if (need) {
-        if (idx < W.n_paths) {
-          g = idx;
-          const int lp = (int)(idx / W.spp_w), s = (int)(idx % W.spp_w);  // pixel-major: g = lp * spp_w + s
-          if (lp >= W.npix || s >= W.spp_w) atomicOr(W.err, 1);
-          const int pix = W.pixels ? W.pixels[lp] : lp;
-          V3 o, d;
-          float tm;
-          camera_ray(S, pix, W.s_base + s, W.sobol[2 * s], W.sobol[2 * s + 1], W.nx, W.ny, W.base_seed, o, d, tm,
-                     rng);
-          r = Ray{o, d, tm};
-          depth = 0;
-          spec = 0;
-          prays = 0;
-        } else {
-          exhausted = true;
-        }
+      if (need && idx < n_paths) {
+        g = (int)idx;
+        // pixel-major: g = lp * spp_w + s
+        const uint32_t lp = idx / (uint32_t)W.spp_w, s = idx - lp * (uint32_t)W.spp_w;
+        if ((int)lp >= W.npix || (int)s >= W.spp_w) atomicOr(W.err, 1);
+        const int pix = W.pixels ? W.pixels[lp] : lp;
+        V3 o, d;
+        float tm;
+        camera_ray(S, pix, W.s_base + s, W.sobol[2 * s], W.sobol[2 * s + 1], W.nx, W.ny, W.base_seed, o, d, tm,
+                   rng);
+        r = Ray{o, d, tm};
+        depth = 0;
       }
     }
-    if (!nxt_armed && pool_end < (unsigned long long)W.n_paths) {  // arm the next chunk
-      if (lane_id() == 0) nxt_lane0 = atomicAdd(W.cursor, (unsigned long long)kPoolChunk);
+    if (!nxt_armed && pool_end < n_paths) {  // arm the next chunk
+      if (lane_id() == 0) nxt_lane0 = (uint32_t)atomicAdd(W.cursor, (unsigned long long)kPoolChunk);
       nxt_armed = true;
     }
     if (__ballot(g >= 0) == 0) break;
@@ -1872,7 +1883,6 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
     float d_pdf = 0;
     int d_tries = 0;
     if (g >= 0) {
-      ++prays;
       const WorldHit w = world_hit<MEDIA, TIMED ? (TR_BVH4_TIMED | (WL ? TR_WL : 0)) : TR>(S, r, rng, cx);
       if (TIMED) {
         const uint64_t t = __builtin_amdgcn_s_memtime();
@@ -1919,8 +1929,7 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
           else if (fam == FAM_BECK) scatter<FAM_BECK>(S, M, r.d, r.tm, h.p, h.n, h.u, h.v, rng, rec, sp, nd, nt);
           else scatter<FAM_SPEC>(S, M, r.d, r.tm, h.p, h.n, h.u, h.v, rng, rec, sp, nd, nt);
           if (depth >= W.max_depth || slot >= W.lanes) atomicOr(W.err, 2);
-          else nts(&W.rec[(size_t)depth * W.lanes + slot], rec);
-          if (sp) spec |= (1ull << depth);
+          else rec_store(&W.rec[(size_t)depth * W.lanes + slot], rec);
           r = Ray{h.p, nd, nt};
           ++depth;
           done = false;
@@ -1933,7 +1942,7 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
       if (c < 0) c = 0;
       const V3 as = d_atten * (c / kPi);
       if (depth >= W.max_depth || slot >= W.lanes) atomicOr(W.err, 2);
-      else nts(&W.rec[(size_t)depth * W.lanes + slot], make_float4(as.x, as.y, as.z, d_pdf));
+      else rec_store(&W.rec[(size_t)depth * W.lanes + slot], make_float4(as.x, as.y, as.z, d_pdf));
       r = Ray{ds.p, d_dir, r.tm};
       ++depth;
     }
@@ -1951,9 +1960,9 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
       if (done) {
         // fold the bounces back to front (Raytracing_n.cpp:69, :94), as finish_path
         for (int k = depth - 1; k >= 0; --k) {
-          const float4 a = ntl(&W.rec[(size_t)k * W.lanes + slot]);
+          const float4 a = rec_load(&W.rec[(size_t)k * W.lanes + slot]);
           const V3 av = v3(a.x, a.y, a.z);
-          if ((spec >> k) & 1) C = av * C;
+          if (__float_as_uint(a.w) == kSpecMark) C = av * C;  // specular: attenuation * color
           else C = v3(0.f) + (av * C) / a.w;
         }
         if (W.raw) {  // kept paths: [pixel][sample of the frame]
@@ -1961,15 +1970,15 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
           W.raw[3 * kq] = C.x;
           W.raw[3 * kq + 1] = C.y;
           W.raw[3 * kq + 2] = C.z;
-          W.rays[kq] = (uint8_t)prays;
+          W.rays[kq] = (uint8_t)(depth + 1);  // world rays of the path
         }
         if (!(C.x == C.x)) C.x = 0;  // de_nan (Raytracing_n.cpp:47-53)
         if (!(C.y == C.y)) C.y = 0;
         if (!(C.z == C.z)) C.z = 0;
-        nts(&W.sample[3 * g], C.x);
-        nts(&W.sample[3 * g + 1], C.y);
-        nts(&W.sample[3 * g + 2], C.z);
-        nrays += prays;
+        nts(&W.sample[3 * (size_t)g], C.x);
+        nts(&W.sample[3 * (size_t)g + 1], C.y);
+        nts(&W.sample[3 * (size_t)g + 2], C.z);
+        nrays += depth + 1;
         g = -1;
       }
       if (TIMED) tp[4] += __builtin_amdgcn_s_memtime() - tq;
