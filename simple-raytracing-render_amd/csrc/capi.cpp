@@ -481,11 +481,12 @@ void srr_image_free(unsigned char* pixels) { free(pixels); }
 
 int srr_device_kat(const char* name, int n, int width, float* records) {
   if (!name || !records || n <= 0 || width <= 0) return fail(SRR_EINVAL, "bad KAT arguments");
-  static const char* kNames[] = {"erf", "beckmann11", "beckmann_dist", "beckmann_pdf", "cosine_pdf",
-                                 "orennayar_pdf", "dielectric", "metal", "triangle", "aabb", "sqrt"};
-  static const int kWidth[] = {3, 5, 16, 21, 21, 21, 14, 14, 26, 15, 2};
+  static const char* kNames[] = {"erf",   "beckmann11", "beckmann_dist", "beckmann_pdf", "cosine_pdf",
+                                 "orennayar_pdf", "dielectric", "metal", "triangle", "aabb", "sqrt",
+                                 "camera", "lights", "light_list"};
+  static const int kWidth[] = {3, 5, 16, 21, 21, 21, 14, 14, 26, 15, 2, 23, 15, 15};
   int kind = -1;
-  for (int k = 0; k < 11; ++k)
+  for (int k = 0; k < 14; ++k)
     if (!strcmp(name, kNames[k])) kind = k;
   if (kind < 0) return fail(SRR_EINVAL, std::string("no device KAT named ") + name);
   if (width != kWidth[kind]) return fail(SRR_EINVAL, std::string("KAT ") + name + ": unexpected record width");
@@ -516,9 +517,54 @@ int srr_device_kat(const char* name, int n, int width, float* records) {
       d.sh.mat = -1;
     }
   }
+  // camera KAT: camera(lookfrom, lookat, (0,1,0), vfov, aspect, aperture, focus, 0, 1) per record, built
+  // by the host scene code exactly as a scene's camera (camera.h:33-48)
+  std::vector<DCamera> cams(kind == 11 ? n : 1);
+  if (kind == 11) {
+    for (int q = 0; q < n; ++q) {
+      const float* r = records + (size_t)q * width;
+      const float vup[3] = {0, 1, 0};
+      Scene cs;
+      cs.camera(r, r + 3, vup, r[6], r[7], r[8], r[9], 0.0f, 1.0f);
+      const HCamera& c = cs.cam;
+      DCamera& d = cams[q];
+      std::memcpy(d.origin, c.origin, 12);
+      std::memcpy(d.llc, c.llc, 12);
+      std::memcpy(d.horizontal, c.horizontal, 12);
+      std::memcpy(d.vertical, c.vertical, 12);
+      std::memcpy(d.u, c.u, 12);
+      std::memcpy(d.v, c.v, 12);
+      d.time0 = c.time0;
+      d.time1 = c.time1;
+      d.lens_radius = c.lens_radius;
+    }
+  }
+  // light KATs: the light list {flip(xz_rect(213,343,227,332,554)), sphere((278,700,280),50),
+  // triangle((150,500,150),(400,520,180),(260,540,420))} of oracle/ref/kat.inc, flattened like a scene's
+  Flat lf;
+  if (kind == 12 || kind == 13) {
+    Scene ls;
+    const int rect = ls.wrap(H_FLIP, ls.rect(H_XZ, 213, 343, 227, 332, 554, -1), nullptr);
+    const float c[3] = {278, 700, 280};
+    const int sph = ls.sphere(c, 50, -1);
+    const float p9[9] = {150, 500, 150, 400, 520, 180, 260, 540, 420};
+    const int tri = ls.triangle(p9, -1, nullptr, nullptr);
+    const int kids[3] = {rect, sph, tri};
+    ls.world = ls.lights = ls.list(kids, 3);
+    const float lf3[3] = {0, 0, -1}, la3[3] = {0, 0, 0}, up[3] = {0, 1, 0};
+    ls.camera(lf3, la3, up, 40, 1, 0, 1, 0, 1);
+    ls.has_camera = true;
+    std::string e;
+    if (flatten(ls, lf, e) < 0 || lf.lights.size() != 3) return fail(SRR_EINVAL, "light KAT scene: " + e);
+  }
   float* d_rec = nullptr;
   float* d_aux = nullptr;
   DStandaloneTri* d_tris = nullptr;
+  DCamera* d_cams = nullptr;
+  DRect* d_rects = nullptr;
+  DSphere* d_sph = nullptr;
+  DStandaloneTri* d_stris = nullptr;
+  DLight* d_lights = nullptr;
   const size_t rb = (size_t)n * width * sizeof(float);
   int rc = 0;
   if (hipMalloc((void**)&d_rec, rb) != hipSuccess || hipMalloc((void**)&d_aux, aux.size() * 4) != hipSuccess ||
@@ -528,12 +574,24 @@ int srr_device_kat(const char* name, int n, int width, float* records) {
               hipMemcpy(d_aux, aux.data(), aux.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
               hipMemcpy(d_tris, tris.data(), tris.size() * sizeof(DStandaloneTri), hipMemcpyHostToDevice) != hipSuccess))
     rc = fail(SRR_EIO, "copy to device failed");
-  if (!rc && launch_kat(kind, n, width, d_rec, d_aux, d_tris) < 0) rc = fail(SRR_EIO, "KAT kernel launch failed");
+  auto upload = [&rc](auto*& dst, const auto& v) {
+    if (rc || v.empty()) return;
+    const size_t b = v.size() * sizeof(v[0]);
+    if (hipMalloc((void**)&dst, b) != hipSuccess) rc = fail(SRR_ENOMEM, "device allocation failed");
+    else if (hipMemcpy(dst, v.data(), b, hipMemcpyHostToDevice) != hipSuccess) rc = fail(SRR_EIO, "copy to device failed");
+  };
+  upload(d_cams, cams);
+  upload(d_rects, lf.rects);
+  upload(d_sph, lf.spheres);
+  upload(d_stris, lf.stris);
+  upload(d_lights, lf.lights);
+  const KatTables kt{d_cams, d_rects, d_sph, d_stris, d_lights, (int)lf.lights.size()};
+  if (!rc && launch_kat(kind, n, width, d_rec, d_aux, d_tris, kt) < 0) rc = fail(SRR_EIO, "KAT kernel launch failed");
   if (!rc && (hipDeviceSynchronize() != hipSuccess || hipMemcpy(records, d_rec, rb, hipMemcpyDeviceToHost) != hipSuccess))
     rc = fail(SRR_EIO, "KAT kernel failed");
-  (void)hipFree(d_rec);
-  (void)hipFree(d_aux);
-  (void)hipFree(d_tris);
+  for (void* p : {(void*)d_rec, (void*)d_aux, (void*)d_tris, (void*)d_cams, (void*)d_rects, (void*)d_sph,
+                  (void*)d_stris, (void*)d_lights})
+    (void)hipFree(p);
   return rc;
 }
 

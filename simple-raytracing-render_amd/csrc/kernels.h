@@ -96,6 +96,7 @@ struct PathWork {
   float4* rec;            // bounce records [max_depth][lanes]
   int lanes;              // persistent lanes (grid * block)
   int* err;               // guard bits set on an out-of-range index (never expected)
+  int stack_cap;          // BVH4 traversal stack entries (kStack = 8; fewer forces the exact re-walk)
 };
 
 constexpr int kPathsWorldLdsBytes = 8192;  // == kernels.hip kWorldLdsBytes
@@ -104,7 +105,18 @@ void dump_trace_timing();
 int paths_lanes_per_device(const SceneView& S, int device);  // persistent grid capacity
 void launch_paths(const SceneView& S, const PathWork& W, int all_families, hipStream_t st);
 // device known-answer tests (srr_device_kat); kind = dev::KatKind
-int launch_kat(int kind, int n, int w, float* d_rec, const float* d_aux, const DStandaloneTri* d_tris);
+// device tables of the camera / light KATs (srr_device_kat builds them with the
+// host scene code: one camera per record, one light list for all records)
+struct KatTables {
+  const DCamera* cams;
+  const DRect* rects;
+  const DSphere* spheres;
+  const DStandaloneTri* stris;
+  const DLight* lights;
+  int n_lights;
+};
+int launch_kat(int kind, int n, int w, float* d_rec, const float* d_aux, const DStandaloneTri* d_tris,
+               const KatTables& kt);
 void launch_accumulate_window(const float* sample, int npix, int spp_w, float* acc, hipStream_t st);
 void launch_raygen(const SceneView& S, const PathState& P, const BatchInfo& B, hipStream_t st);
 void launch_trace(const SceneView& S, const PathState& P, const int* active, const int* count, int max_n,

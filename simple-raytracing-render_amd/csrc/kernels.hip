@@ -209,7 +209,7 @@ SRR_D T wload(const T* p, int i) {
 constexpr int kTraceBlock = 256;
 constexpr int kStack = 8;  // LDS stack entries per ray; deeper -> exact BVH2 re-walk
 constexpr int kWorldLdsBytes = kPathsWorldLdsBytes;  // world tables staged in LDS up to this size
-constexpr unsigned long long kTimingCap = 1 << 16;  // SRR_TIMING wave records  // LDS stack entries per ray; deeper -> exact BVH2 re-walk
+constexpr unsigned long long kTimingCap = 1 << 16;  // SRR_TIMING wave records
 
 struct TraceCtx {
   unsigned long long* ctr;  // optional counters: boxes tested, triangle tests, stack overflows
@@ -217,6 +217,8 @@ struct TraceCtx {
   float* st_t;     // entry distance of each stacked node
   const __attribute__((address_space(3))) f32x4* lds_nodes = nullptr;  // LDS copy of node4[0, lds_count) (k_paths)
   int lds_count = 0;
+  int st_cap = kStack;                   // stack entries used (<= kStack; SRR_STACK_CAP tests the re-walk)
+  unsigned long long* ovf = nullptr;     // optional: += 1 per traversal that overflowed into the re-walk
   // SRR_TIMING diagnostics (wave-uniform): cycles inside mesh traversals, steps
   mutable uint64_t mesh_cycles = 0;
   mutable int mesh_steps = 0;
@@ -338,7 +340,7 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
 #pragma unroll
       for (int c = 3; c >= 1; --c) {
         if (kn[c] < 0) continue;
-        if (sp < kStack) {
+        if (sp < cx.st_cap) {
           cx.st_node[sp * kTraceBlock] = kn[c];
           cx.st_t[sp * kTraceBlock] = kt[c];
           ++sp;
@@ -375,7 +377,10 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
     cx.mesh_steps += st;
     cx.mesh_cycles += __builtin_amdgcn_s_memtime() - tm_enter;
   }
-  if (overflow) return mesh_hit<false>(S, m, r, tmin, tmax, is_medium, out, cx.ctr);  // rare: exact re-walk
+  if (overflow) {  // rare: exact re-walk
+    if (cx.ovf) atomicAdd(cx.ovf, 1ull);
+    return mesh_hit<false>(S, m, r, tmin, tmax, is_medium, out, cx.ctr);
+  }
   out.t = best_t;
   out.tri = best_i;
   return found;
@@ -1064,9 +1069,8 @@ SRR_D float lights_pdf(const SceneView& S, V3 o, V3 v) {
 
 __device__ __noinline__ V3 light_random_other(const SceneView& S, const DLight& L, V3 o, Rng& rng);
 
-SRR_D V3 lights_random(const SceneView& S, V3 o, Rng& rng) {
-  int index = int(drand(rng) * S.n_lights);
-  const DLight& L = S.lights[index];
+// one light's random() (aarect.h:57-60, sphere.h:80-86, triangle.h:89-94)
+SRR_D V3 light_random_one(const SceneView& S, const DLight& L, V3 o, Rng& rng) {
   if (L.kind == LIGHT_XZRECT) {  // aarect.h:57-60: z drawn before x
     const DRect& q = S.rects[L.idx];
     float z = q.lo1 + drand(rng) * (q.hi1 - q.lo1);
@@ -1075,6 +1079,12 @@ SRR_D V3 lights_random(const SceneView& S, V3 o, Rng& rng) {
   }
   if (L.kind == LIGHT_NONE) return v3(1, 0, 0);
   return light_random_other(S, L, o, rng);
+}
+
+// hitable_list::random over the light list (hitable_list.h:63-67)
+SRR_D V3 lights_random(const SceneView& S, V3 o, Rng& rng) {
+  int index = int(drand(rng) * S.n_lights);
+  return light_random_one(S, S.lights[index], o, rng);
 }
 
 __device__ __noinline__ V3 light_random_other(const SceneView& S, const DLight& L, V3 o, Rng& rng) {
@@ -1394,6 +1404,25 @@ SRR_D void coop_mixture(const SceneView& S, const DiffSetup& me, bool& pend, int
   }
 }
 
+// camera::get_ray(s, t) (camera.h:51-59; random_in_unit_disk camera.h:8-14)
+SRR_D void camera_get_ray(const DCamera& C, float u, float v, Rng& rng, V3& o, V3& dir, float& time) {
+  V3 pd;
+  do {  // random_in_unit_disk (camera.h:8-14): y drawn before x
+    float y = drand(rng);
+    float x = drand(rng);
+    pd = 2.0f * v3(x, y, 0) - v3(1, 1, 0);
+  } while (dot(pd, pd) >= 1.0);
+  V3 rd = C.lens_radius * pd;
+  V3 cu = v3(C.u[0], C.u[1], C.u[2]), cv = v3(C.v[0], C.v[1], C.v[2]);
+  V3 offset = cu * rd.x + cv * rd.y;
+  time = C.time0 + drand(rng) * (C.time1 - C.time0);
+  V3 org = v3(C.origin[0], C.origin[1], C.origin[2]);
+  dir = v3(C.llc[0], C.llc[1], C.llc[2]) + u * v3(C.horizontal[0], C.horizontal[1], C.horizontal[2]) +
+        v * v3(C.vertical[0], C.vertical[1], C.vertical[2]) - org - offset;
+  dir = unit_vector(dir);
+  o = org + offset;
+}
+
 // The camera ray of sample s_global of pixel `pix` with its per-path RNG streams
 // (SURVEY §8(d) seeding; Raytracing_n.cpp:827-836; camera::get_ray, camera.h:51-59).
 SRR_D void camera_ray(const SceneView& S, int pix, int s_global, double sx, double sy, int nx, int ny,
@@ -1411,23 +1440,9 @@ SRR_D void camera_ray(const SceneView& S, int pix, int s_global, double sx, doub
   rng.pcg = 0x853c49e6748fea9bULL ^ (rng.lcg << 16);
   float u = float(sx + i) / float(nx);
   float v = float(sy + j) / float(ny);
-  const DCamera& C = *S.cam;
-  V3 pd;
-  do {  // random_in_unit_disk (camera.h:8-14): y drawn before x
-    float y = drand(rng);
-    float x = drand(rng);
-    pd = 2.0f * v3(x, y, 0) - v3(1, 1, 0);
-  } while (dot(pd, pd) >= 1.0);
-  V3 rd = C.lens_radius * pd;
-  V3 cu = v3(C.u[0], C.u[1], C.u[2]), cv = v3(C.v[0], C.v[1], C.v[2]);
-  V3 offset = cu * rd.x + cv * rd.y;
-  time = C.time0 + drand(rng) * (C.time1 - C.time0);
-  V3 org = v3(C.origin[0], C.origin[1], C.origin[2]);
-  dir = v3(C.llc[0], C.llc[1], C.llc[2]) + u * v3(C.horizontal[0], C.horizontal[1], C.horizontal[2]) +
-        v * v3(C.vertical[0], C.vertical[1], C.vertical[2]) - org - offset;
-  dir = unit_vector(dir);
-  o = org + offset;
+  camera_get_ray(*S.cam, u, v, rng, o, dir, time);
 }
+
 
 __global__ void __launch_bounds__(256) k_raygen(SceneView S, PathState P, BatchInfo B) {
   int q = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1806,6 +1821,8 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
   TraceCtx cx{nullptr, s_node + threadIdx.x, s_t + threadIdx.x};
   cx.lds_nodes = (const __attribute__((address_space(3))) f32x4*)s_n4;
   cx.lds_count = S0.node4_lds;
+  cx.st_cap = W.stack_cap;
+  cx.ovf = W.counters + 11;
   const int slot = blockIdx.x * blockDim.x + threadIdx.x;
   int g = -1;  // path of this lane (a window numbers its paths below 2^31), -1 idle
   const uint32_t n_paths = (uint32_t)W.n_paths;
@@ -2143,7 +2160,7 @@ __global__ void k_finish(const float* acc, float* mean, int64_t n, int ns) {
 // test can compare them bit for bit with the reference's outputs.
 // aux: 4 host-computed floats per record (Beckmann alphas, Oren-Nayar A / B).
 enum KatKind : int { KAT_ERF, KAT_BECK11, KAT_BECK_DIST, KAT_BECK_PDF, KAT_COSINE, KAT_ORENNAYAR, KAT_DIELECTRIC,
-                     KAT_METAL, KAT_TRIANGLE, KAT_AABB, KAT_SQRT };
+                     KAT_METAL, KAT_TRIANGLE, KAT_AABB, KAT_SQRT, KAT_CAMERA, KAT_LIGHTS, KAT_LIGHT_LIST };
 
 SRR_D V3 kat3(const float* p) { return v3(p[0], p[1], p[2]); }
 SRR_D void kat_put3(float* p, V3 v) { p[0] = v.x, p[1] = v.y, p[2] = v.z; }
@@ -2158,7 +2175,7 @@ SRR_D void kat_put_pcg(float* p, uint64_t s) {
   for (int k = 0; k < 4; ++k) p[k] = (float)((s >> (16 * k)) & 0xFFFF);
 }
 
-__global__ void k_kat(int kind, int n, int w, float* rec, const float* aux, const DStandaloneTri* tris) {
+__global__ void k_kat(int kind, int n, int w, float* rec, const float* aux, const DStandaloneTri* tris, KatTables kt) {
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= n) return;
   float* r = rec + (size_t)q * w;
@@ -2263,6 +2280,47 @@ __global__ void k_kat(int kind, int n, int w, float* rec, const float* aux, cons
     case KAT_SQRT:
       r[1] = rsqrt_exact(r[0]);
       break;
+    case KAT_CAMERA: {  // in: lookfrom lookat vfov aspect aperture focus s t lcg | out: origin dir time lcg
+      Rng rng{kat_lcg(r + 12), 0};
+      V3 o, d;
+      float tm;
+      camera_get_ray(kt.cams[q], r[10], r[11], rng, o, d, tm);
+      kat_put3(r + 14, o);
+      kat_put3(r + 17, d);
+      r[20] = tm;
+      kat_put_lcg(r + 21, rng.lcg);
+      break;
+    }
+    case KAT_LIGHTS:        // in: o lcg | out: rect dir, pdf; sphere dir, pdf; lcg
+    case KAT_LIGHT_LIST: {  // in: o lcg | out: list dir, list pdf; triangle dir, pdf; lcg
+      SceneView S{};
+      S.rects = kt.rects;
+      S.spheres = kt.spheres;
+      S.stris = kt.stris;
+      S.lights = kt.lights;
+      S.n_lights = kt.n_lights;
+      Rng rng{kat_lcg(r + 3), 0};
+      const V3 o = kat3(r);
+      V3 d1, d2;
+      float p1, p2;
+      if (kind == KAT_LIGHTS) {  // the list's first two lights on their own: flip(xz_rect), sphere
+        d1 = light_random_one(S, kt.lights[0], o, rng);
+        p1 = light_pdf_one(S, kt.lights[0], o, d1);
+        d2 = light_random_one(S, kt.lights[1], o, rng);
+        p2 = light_pdf_one(S, kt.lights[1], o, d2);
+      } else {  // the whole list (hitable_list::random / pdf_value), then its triangle alone
+        d1 = lights_random(S, o, rng);
+        p1 = lights_pdf(S, o, d1);
+        d2 = light_random_one(S, kt.lights[2], o, rng);
+        p2 = light_pdf_one(S, kt.lights[2], o, d2);
+      }
+      kat_put3(r + 5, d1);
+      r[8] = p1;
+      kat_put3(r + 9, d2);
+      r[12] = p2;
+      kat_put_lcg(r + 13, rng.lcg);
+      break;
+    }
     case KAT_AABB: {
       const V3 d = kat3(r + 9);
       r[14] = slab(make_float4(r[0], r[1], r[2], 0), make_float4(r[3], r[4], r[5], 0), kat3(r + 6),
@@ -2466,8 +2524,9 @@ void launch_paths(const SceneView& S, const PathWork& W, int all_families, hipSt
 #undef SRR_LAUNCH_PATHS
 }
 
-int launch_kat(int kind, int n, int w, float* d_rec, const float* d_aux, const DStandaloneTri* d_tris) {
-  hipLaunchKernelGGL(dev::k_kat, dim3((n + 63) / 64), dim3(64), 0, 0, kind, n, w, d_rec, d_aux, d_tris);
+int launch_kat(int kind, int n, int w, float* d_rec, const float* d_aux, const DStandaloneTri* d_tris,
+               const KatTables& kt) {
+  hipLaunchKernelGGL(dev::k_kat, dim3((n + 63) / 64), dim3(64), 0, 0, kind, n, w, d_rec, d_aux, d_tris, kt);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

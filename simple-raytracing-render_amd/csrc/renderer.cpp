@@ -339,6 +339,8 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
     w.rec = r->pw_rec;
     w.err = (int*)(r->pw_ctr + 2);
     w.lanes = (int)std::min<int64_t>(r->pw_lanes, ((w.n_paths + 255) / 256) * 256);
+    w.stack_cap = 8;  // kernels.hip kStack
+    if (const char* e = getenv("SRR_STACK_CAP")) w.stack_cap = std::max(1, std::min(8, atoi(e)));
     RCHK(hipMemsetAsync(w.cursor, 0, sizeof(unsigned long long), st));
     RCHK(hipEventRecord(r->lanes[0].ev_t0, st));
     launch_paths(r->view, w, all_fam ? 1 : 0, st);
@@ -372,6 +374,7 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
   float total = 0;
   RCHK(hipEventElapsedTime(&total, r->ev_beg, r->ev_end));
   s.world_rays = (int64_t)rays;
+  s.stack_overflows = (int64_t)ctr[11];
   s.paths = npix * p->spp;
   s.trace_ms = kernel_ms;
   s.total_ms = total;

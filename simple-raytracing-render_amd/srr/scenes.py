@@ -112,6 +112,24 @@ def s5_soldier_fog(divs: int = 40) -> tuple[Scene, dict]:
     return s4_soldier_standin(divs=divs, fog=True)
 
 
+def s6_mixed_lights() -> tuple[Scene, dict]:
+    """Cornell box lit by its ceiling rect, an emissive sphere and an emissive
+    triangle, all three in the light list (hlist): exercises hitable_list's light
+    selection (hitable_list.h:54-67) and the sphere and triangle light pdfs
+    (sphere.h:69-86, triangle.h:70-94) next to the xz_rect's (aarect.h:45-60)."""
+    sc = Scene()
+    objs, _ = _cornell(sc)
+    glow = sc.diffuse_light(sc.constant_texture(8.0))
+    tri_p = ((150, 500, 150), (400, 520, 180), (260, 540, 420))
+    objs.append(sc.sphere((420, 380, 380), 45, glow))
+    objs.append(sc.triangle(*tri_p, glow))
+    sc.set_world(sc.hitable_list(objs))
+    sc.camera((278, 278, -800), (278, 278, 0), (0, 1, 0), 40.0, 1.0, 0.0, 10.0, 0.0, 1.0)
+    sc.set_lights(sc.hitable_list([sc.flip_normals(sc.xz_rect(213, 343, 227, 332, 554)),
+                                   sc.sphere((420, 380, 380), 45), sc.triangle(*tri_p)]))
+    return sc, dict(nx=256, ny=256, spp=64, max_depth=50)
+
+
 SCENES = {
     "s1": s1_cornell,
     "s2": s2_cornell_teapot,
@@ -119,4 +137,5 @@ SCENES = {
     "s3_metal": lambda: s3_cornell_teapot_microfacet("metal"),
     "s4": s4_soldier_standin,
     "s5": s5_soldier_fog,
+    "s6": s6_mixed_lights,
 }

@@ -31,11 +31,16 @@ RENDERS = [
     ("s4_small", lambda: scenes.s4_soldier_standin(divs=8)[0], 32, 18, 8, 50),
     ("s5_small", lambda: scenes.s4_soldier_standin(divs=8, fog=True)[0], 32, 18, 8, 50),
     ("s2_depth3", lambda: scenes.s2_cornell_teapot()[0], 16, 16, 8, 3),
+    # sphere and triangle lights next to the rect in the light list
+    ("s6_lights", lambda: scenes.s6_mixed_lights()[0], 32, 32, 16, 50),
+    # C4 / C5 stand-ins at their configured mesh (divs 40: 102,400 triangles)
+    ("s4_d40", lambda: scenes.s4_soldier_standin(divs=40)[0], 64, 36, 4, 50),
+    ("s5_d40", lambda: scenes.s4_soldier_standin(divs=40, fog=True)[0], 64, 36, 4, 50),
 ]
 
 KATS = [("erf", 512), ("beckmann11", 512), ("beckmann_dist", 512), ("beckmann_pdf", 512), ("cosine_pdf", 256),
         ("orennayar_pdf", 256), ("dielectric", 256), ("metal", 256), ("triangle", 1024), ("aabb", 1024),
-        ("camera", 256), ("lights", 256)]
+        ("camera", 256), ("lights", 256), ("light_list", 256)]
 
 
 def run(*args):

@@ -1,6 +1,7 @@
 """Device known-answer tests: the HIP implementations of the reference's
 per-function code (material.h, pdf.h, microfacet_distribution.h, common.h,
-triangle.h, aabb.h), run through srr_device_kat on the reference's own KAT
+triangle.h, aabb.h, camera.h, light sampling of aarect.h / sphere.h / triangle.h /
+hitable_list.h), run through srr_device_kat on the reference's own KAT
 records (tests/golden/kat_*.bin, made by oracle/ref from the reference's
 functions), must reproduce the reference's outputs bit for bit."""
 import ctypes
@@ -15,7 +16,8 @@ from srr import capi
 OUT = {"erf": range(1, 3), "beckmann11": range(3, 5), "beckmann_dist": range(7, 16),
        "beckmann_pdf": range(12, 21), "cosine_pdf": list(range(9, 16)) + [19, 20],
        "orennayar_pdf": list(range(9, 16)) + [19, 20], "dielectric": range(9, 14), "metal": range(9, 14),
-       "triangle": range(16, 26), "aabb": [14]}
+       "triangle": range(16, 26), "aabb": [14], "camera": range(14, 23), "lights": range(5, 15),
+       "light_list": range(5, 15)}
 
 
 def device_kat(name, rec):
