@@ -7,11 +7,13 @@
 
 One step = one whole frame through the C-ABI (srr_render_device, inputs
 resident in HBM) on every rank, then the frame-end exchange over RCCL
-(srr/dist.py).  Default plan "samples" (weak scaling): each GPU
-renders the BASELINE config's 512x512x1024 paths as its sample range of one
-N*1024-spp frame; one reduce of per-pixel sums to rank 0.  Plan "tiles"
-(strong scaling): 32x32 tiles round-robin, one all_gather.  A "sample" is one world ray segment
-(one reference world->hit call).  Rank 0 prints one JSON line.
+(srr/dist.py).  Default plan "tiles" (strong scaling, the
+north_star split): the BASELINE config's one 512x512x1024 frame, 32x32 tiles
+round-robin over the N GPUs, one gather of the tiles' means to rank 0 (the
+image is bitwise the 1-GPU image).  Plan "samples" (weak scaling): each GPU
+renders 512x512x1024 paths as its sample range of one N*1024-spp frame; one
+reduce of raw per-pixel sums.  A "sample" is one world ray segment (one
+reference world->hit call).  Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
@@ -38,9 +40,10 @@ def parse():
     ap.add_argument("--ny", type=int, default=0)
     ap.add_argument("--spp", type=int, default=0)
     ap.add_argument("--batch-paths", type=int, default=0)
-    ap.add_argument("--plan", default="samples", choices=["samples", "tiles"],
-                    help="multi-GPU split: samples = weak scaling (each GPU renders spp samples of every "
-                         "pixel, one reduce), tiles = strong scaling (32x32 tiles round-robin, one all_gather)")
+    ap.add_argument("--plan", default="tiles", choices=["tiles", "samples"],
+                    help="multi-GPU split: tiles = strong scaling, the north_star split (one frame, 32x32 tiles "
+                         "round-robin, one gather to rank 0; bitwise the 1-GPU image), samples = weak scaling "
+                         "(each GPU renders spp samples of every pixel, one reduce of raw sums)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--count-visits", action="store_true", help="diagnostic: count mesh box/triangle tests (slower)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -169,7 +172,7 @@ def main():
             "dtype": "f32",
             "data": "synthetic (scene built in code: Cornell box + tessellated Utah teapot)",
             "config": {"workload": f"{key}: {a.scene} {nx}x{ny} {spp}spp maxDepth {cfg['max_depth']}" + (
-                                   f", 32x32 tiles round-robin over {world} GPU(s), RCCL all_gather at frame end"
+                                   f", 32x32 tiles round-robin over {world} GPU(s), RCCL gather to rank 0 at frame end"
                                    if a.plan == "tiles" else
                                    f" per GPU; {world} GPU(s) render sample ranges of one {spp * world}spp frame, "
                                    f"RCCL reduce at frame end"),

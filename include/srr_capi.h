@@ -156,6 +156,9 @@ typedef struct srr_params {
                                   /* samples to the renderer's per-pixel running   */
                                   /* sums (set sample_begin to the samples already */
                                   /* in them); the mean covers all of them         */
+#define SRR_FLAG_SUMS 32          /* srr_render_device writes the per-pixel sample */
+                                  /* SUMS (the running sums) instead of the means: */
+                                  /* sample-sharded frames reduce these over ranks */
 
 typedef struct srr_stats {
   int64_t world_rays;   /* world->hit calls (the metric's samples)             */

@@ -353,7 +353,10 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
     s.trace_launches += 1;
   }
   const int64_t acc_total = r->acc_samples + p->spp;
-  launch_finish(r->acc, d_mean, npix, (int)acc_total, st);
+  if (p->flags & SRR_FLAG_SUMS)
+    RCHK(hipMemcpyAsync(d_mean, r->acc, 3 * (size_t)npix * sizeof(float), hipMemcpyDeviceToDevice, st));
+  else
+    launch_finish(r->acc, d_mean, npix, (int)acc_total, st);
   RCHK(hipEventRecord(r->ev_end, st));
   RCHK(hipStreamSynchronize(st));
   RCHK(hipGetLastError());
@@ -604,7 +607,10 @@ int render_device(srr_renderer* r, const srr_params* p, const int32_t* pix, int6
     if (!progress) std::this_thread::yield();
   }
   const int64_t acc_total = r->acc_samples + p->spp;
-  launch_finish(r->acc, d_mean, npix, (int)acc_total, ast);
+  if (p->flags & SRR_FLAG_SUMS)
+    RCHK(hipMemcpyAsync(d_mean, r->acc, 3 * (size_t)npix * sizeof(float), hipMemcpyDeviceToDevice, ast));
+  else
+    launch_finish(r->acc, d_mean, npix, (int)acc_total, ast);
   RCHK(hipEventRecord(r->ev_end, ast));
   RCHK(hipStreamSynchronize(ast));
   RCHK(hipGetLastError());

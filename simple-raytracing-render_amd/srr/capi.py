@@ -18,6 +18,7 @@ FLAG_KEEP_PATHS = 2
 FLAG_COUNT_VISITS = 4
 FLAG_WAVEFRONT = 8
 FLAG_CONTINUE = 16
+FLAG_SUMS = 32
 
 
 class SrrError(RuntimeError):

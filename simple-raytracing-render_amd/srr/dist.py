@@ -4,16 +4,18 @@
 Every (pixel, sample) path is independent and the scene is read-only, so a
 frame shards with no exchange until the end.  Two plans:
 
-* ``tiles``   (strong scaling, a fixed frame): rank k renders the 32x32 tiles
-  t with t % world == k, all samples.  Frame end: one all_gather of the packed
-  per-pixel means; rank 0 scatters them into the image.  Bitwise equal to the
-  one-GPU image (each pixel's samples are summed on one GPU in sample order).
+* ``tiles``   (strong scaling, a fixed frame; the default): rank k renders the
+  32x32 tiles t with t % world == k, all samples.  Frame end: one gather of
+  the packed per-pixel means to rank 0, which scatters them into the image.
+  Bitwise equal to the one-GPU image (each pixel's samples are summed on one
+  GPU in sample order).
 * ``samples`` (weak scaling, fixed work per GPU): rank k renders every pixel
   with samples [k*spp, (k+1)*spp) of one frame of world*spp samples per pixel
   (the per-path seeds and Sobol points are the global sample index's, so
-  rank 0's slice is exactly the one-GPU spp frame).  Frame end: one reduce of
-  the per-pixel sample sums to rank 0.  Equal to the one-GPU world*spp frame up
-  to float summation order (partial sums per rank).
+  rank 0's slice is exactly the one-GPU spp frame).  Each rank outputs its raw
+  per-pixel sample sums (SRR_FLAG_SUMS); frame end: one reduce(sum) to rank 0,
+  which takes the mean as the renderer does (sum * (1/ns)).  Equal to the
+  one-GPU world*spp frame up to float summation order (partial sums per rank).
 """
 from __future__ import annotations
 
@@ -50,8 +52,8 @@ def plan_shard(nx, ny, spp, max_depth, rank, world, plan="tiles", tile=32, batch
         counts = [capi.shard_pixels(capi.make_params(nx, ny, spp, shard=(k, world), tile=tile)).size
                   for k in range(world)]
         return Shard(rank, world, plan, p, capi.shard_pixels(p), counts, spp)
-    p = capi.make_params(nx, ny, spp, max_depth, shard=(0, 1), tile=tile, batch_paths=batch_paths, flags=flags,
-                         sample_begin=rank * spp)
+    p = capi.make_params(nx, ny, spp, max_depth, shard=(0, 1), tile=tile, batch_paths=batch_paths,
+                         flags=flags | capi.FLAG_SUMS, sample_begin=rank * spp)
     return Shard(rank, world, plan, p, np.arange(nx * ny, dtype=np.int32), [nx * ny] * world, spp * world)
 
 
@@ -66,9 +68,10 @@ def shard_pixels_of(sh: Shard, k: int) -> np.ndarray:
 class FrameExchange:
     """Frame-end exchange for one plan, with buffers allocated once.
 
-    `local` is this rank's [n_max, 3] float32 tensor of per-pixel means (rows
-    beyond its pixel count are ignored).  `finish()` returns the assembled
-    [nx*ny, 3] frame of means on rank 0 (None elsewhere)."""
+    `local` is this rank's [n_max, 3] float32 tensor of per-pixel means
+    (``tiles``; rows beyond its pixel count are ignored) or sample sums
+    (``samples``).  `finish()` returns the assembled [nx*ny, 3] frame of means
+    on rank 0 (None elsewhere)."""
 
     def __init__(self, sh: Shard, device, dist=None):
         import torch
@@ -78,29 +81,28 @@ class FrameExchange:
         self.local = torch.zeros((self.n_max, 3), dtype=torch.float32, device=device)
         self.image = torch.zeros((nx * ny, 3), dtype=torch.float32, device=device)
         if sh.plan == "tiles":
-            self.gathered = [torch.zeros_like(self.local) for _ in range(sh.world)]
+            self.gathered = [torch.zeros_like(self.local) for _ in range(sh.world)] if sh.rank == 0 else None
             self.idx = [torch.from_numpy(shard_pixels_of(sh, k).astype(np.int64)).to(device)
                         for k in range(sh.world)]
+        # the renderer's mean: sum * (float)(1.0 / (float)ns)  (kernels.hip k_finish)
+        self.inv_ns = torch.tensor(np.float32(1.0 / float(np.float32(sh.total_spp))), device=device)
 
     def finish(self):
         sh, torch = self.sh, self.torch
-        if sh.world == 1:
-            if sh.plan == "tiles":
-                self.image[self.idx[0]] = self.local[:sh.counts[0]]
-            else:
-                self.image.copy_(self.local)
-            return self.image
         if sh.plan == "tiles":
-            self.dist.all_gather(self.gathered, self.local)  # one exchange over RCCL / xGMI
+            if sh.world == 1:
+                self.image[self.idx[0]] = self.local[:sh.counts[0]]
+                return self.image
+            self.dist.gather(self.local, self.gathered, dst=0)  # one exchange over RCCL / xGMI
             if sh.rank != 0:
                 return None
             for k in range(sh.world):
                 self.image[self.idx[k]] = self.gathered[k][:sh.counts[k]]
             return self.image
-        # samples: per-pixel sums of this rank's samples, reduced to rank 0
-        self.local.mul_(float(sh.params.spp))
-        self.dist.reduce(self.local, dst=0)
-        if sh.rank != 0:
-            return None
-        torch.div(self.local, float(sh.total_spp), out=self.image)
+        # samples: raw per-pixel sums of this rank's samples, reduced to rank 0
+        if sh.world > 1:
+            self.dist.reduce(self.local, dst=0)
+            if sh.rank != 0:
+                return None
+        torch.mul(self.local, self.inv_ns, out=self.image)
         return self.image

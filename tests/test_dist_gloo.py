@@ -40,8 +40,11 @@ def _rank_main(rank, world, port, plan, text, outdir):
             ex.local[:sh.pixels.size] = torch.from_numpy(r["img"])
         else:
             full = ob.render(text, NX, NY, SPP * world, 50, want_paths=True)
-            mine = full["paths"][:, rank * SPP:(rank + 1) * SPP, :]
-            ex.local[:] = torch.from_numpy(mine.sum(axis=1, dtype=np.float32) / np.float32(SPP))
+            mine = np.nan_to_num(full["paths"][:, rank * SPP:(rank + 1) * SPP, :], nan=0.0)  # de_nan
+            acc = np.zeros((NX * NY, 3), np.float32)
+            for k in range(SPP):  # the renderer's raw running sums (SRR_FLAG_SUMS), in sample order
+                acc += mine[:, k]
+            ex.local[:] = torch.from_numpy(acc)
         img = ex.finish()
         if rank == 0:
             np.save(os.path.join(outdir, f"{plan}.npy"), img.numpy())
@@ -49,10 +52,11 @@ def _rank_main(rank, world, port, plan, text, outdir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("plan", ["tiles", "samples"])
-def test_two_rank_frame_matches_single_render(plan, tmp_path):
+@pytest.mark.parametrize("plan,world", [("tiles", 2), ("tiles", 3), ("samples", 2)])
+def test_multi_rank_frame_matches_single_render(plan, world, tmp_path):
+    """tiles: the gathered frame is bitwise the one-renderer frame; samples: the
+    reduced raw sums give the world*spp frame up to summation order."""
     text = _scene_text()
-    world = 2
     mp.spawn(_rank_main, args=(world, _free_port(), plan, text, str(tmp_path)), nprocs=world, join=True)
     img = np.load(tmp_path / f"{plan}.npy")
     if plan == "tiles":
