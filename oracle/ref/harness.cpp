@@ -295,7 +295,9 @@ inline uint32_t canon_bits(float f) {
   return (f != f) ? 0x7fc00000u : u;
 }
 
-// sums <scene.txt> <nx> <ny> <ns> <maxdepth> <pix0> <pix1> <out_prefix>
+// sums <scene.txt> <nx> <ny> <ns> <maxdepth> <pix0> <pix1> <out_prefix> [stride]
+// (pixels pix0, pix0 + stride, ... below pix1; out_prefix "-" writes no files:
+// bench.py's cpu_baseline times the reference this way, one process per core)
 int cmd_sums(int argc, char** argv) {
   if (argc < 10) return 2;
   RefScene S = build(srr_text::parse(srr_text::read_file(argv[2])));
@@ -305,11 +307,14 @@ int cmd_sums(int argc, char** argv) {
   maxDepth = atoi(argv[6]);
   const int p0 = atoi(argv[7]), p1 = atoi(argv[8]);
   const std::string out = argv[9];
+  const int stride = argc > 10 ? std::max(1, atoi(argv[10])) : 1;
   counting_world cw(S.world);
   double** sp = sobol(ns);
   std::vector<uint32_t> rays, hash;
   std::vector<float> mean;
-  for (int pix = p0; pix < p1; ++pix) {
+  auto t0 = std::chrono::steady_clock::now();
+  int npx = 0;
+  for (int pix = p0; pix < p1; pix += stride, ++npx) {
     int i = pix % nx;
     int j = ny - 1 - pix / nx;
     vec3 col(0, 0, 0);
@@ -332,10 +337,13 @@ int cmd_sums(int argc, char** argv) {
     hash.push_back(h);
     for (int c = 0; c < 3; ++c) mean.push_back(col[c]);
   }
-  write(out + ".rays.u32", rays.data(), rays.size() * 4);
-  write(out + ".hash.u32", hash.data(), hash.size() * 4);
-  write(out + ".mean.f32", mean.data(), mean.size() * 4);
-  printf("{\"pixels\": %d, \"world_rays\": %lld}\n", p1 - p0, cw.n);
+  double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (out != "-") {
+    write(out + ".rays.u32", rays.data(), rays.size() * 4);
+    write(out + ".hash.u32", hash.data(), hash.size() * 4);
+    write(out + ".mean.f32", mean.data(), mean.size() * 4);
+  }
+  printf("{\"pixels\": %d, \"world_rays\": %lld, \"ms\": %.3f}\n", npx, cw.n, ms);
   return 0;
 }
 
