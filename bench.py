@@ -36,6 +36,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--scene", default="s2", choices=["s1", "s2", "s3", "s3_metal", "s4", "s5"])
+    ap.add_argument("--divs", type=int, default=0,
+                    help="teapot subdivision (s2/s3: 10 = 6,400 tris; 100 = the reference's as-shipped 640,000, "
+                         "teapot.h:77; s4/s5: 40 = 102,400)")
     ap.add_argument("--nx", type=int, default=0)
     ap.add_argument("--ny", type=int, default=0)
     ap.add_argument("--spp", type=int, default=0)
@@ -138,9 +141,13 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    fac = {"s1": scenes.s1_cornell, "s2": scenes.s2_cornell_teapot, "s3": scenes.s3_cornell_teapot_microfacet,
-           "s3_metal": lambda: scenes.s3_cornell_teapot_microfacet("metal"), "s4": scenes.s4_soldier_standin,
-           "s5": scenes.s5_soldier_fog}[a.scene]
+    dv = {"divs": a.divs} if a.divs else {}
+    if a.divs and a.scene == "s1":
+        raise SystemExit("--divs: s1 has no teapot")
+    fac = {"s1": scenes.s1_cornell, "s2": lambda: scenes.s2_cornell_teapot(**dv),
+           "s3": lambda: scenes.s3_cornell_teapot_microfacet(**dv),
+           "s3_metal": lambda: scenes.s3_cornell_teapot_microfacet("metal", **dv),
+           "s4": lambda: scenes.s4_soldier_standin(**dv), "s5": lambda: scenes.s5_soldier_fog(**dv)}[a.scene]
     sc, cfg = fac()
     nx, ny, spp = a.nx or cfg["nx"], a.ny or cfg["ny"], a.spp or cfg["spp"]
     text = sc.text()
@@ -188,6 +195,11 @@ def main():
     if rank == 0:
         counts_json = json.load(open(os.path.join(ROOT, "tests", "golden", "traversal_counts.json")))
         key = CONFIG_KEY[a.scene]
+        default_divs = {"s2": 10, "s3": 10, "s3_metal": 10, "s4": 40, "s5": 40}.get(a.scene)
+        if a.divs and a.divs != default_divs:
+            key = f"{key}_d{a.divs}"
+        if key not in counts_json:
+            raise SystemExit(f"no reference traversal counts for {key}: add it to tests/golden/make_counts.py")
         b_cfg = counts_json[key]["B_cfg"]
         value = rays_total / elapsed / 1e6
         # roofline of the dominant kernel (srr_trace) on rank 0: algorithmic bytes
@@ -215,7 +227,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (scene built in code: Cornell box + tessellated Utah teapot)",
-            "config": {"workload": f"{key}: {a.scene} {nx}x{ny} {spp}spp maxDepth {cfg['max_depth']}" + (
+            "config": {"workload": f"{key}: {a.scene}{f' divs {a.divs}' if a.divs else ''} {nx}x{ny} {spp}spp "
+                                   f"maxDepth {cfg['max_depth']}" + (
                                    f", 32x32 tiles round-robin over {world} GPU(s), RCCL gather to rank 0 at frame end"
                                    if a.plan == "tiles" else
                                    f" per GPU; {world} GPU(s) render sample ranges of one {spp * world}spp frame, "

@@ -28,6 +28,8 @@ CONFIGS = {
     "C3_metal": (lambda: scenes.s3_cornell_teapot_microfacet("metal"), 96, 96, 16),
     "C4": (scenes.s4_soldier_standin, 192, 108, 8),
     "C5": (scenes.s5_soldier_fog, 192, 108, 8),
+    # C2 with the reference's as-shipped teapot (teapot.h:77: divs 100, 640,000 triangles)
+    "C2_d100": (lambda: scenes.s2_cornell_teapot(divs=100), 96, 96, 16),
 }
 
 

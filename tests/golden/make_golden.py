@@ -31,6 +31,8 @@ RENDERS = [
     ("s4_small", lambda: scenes.s4_soldier_standin(divs=8)[0], 32, 18, 8, 50),
     ("s5_small", lambda: scenes.s4_soldier_standin(divs=8, fog=True)[0], 32, 18, 8, 50),
     ("s2_depth3", lambda: scenes.s2_cornell_teapot()[0], 16, 16, 8, 3),
+    # the reference's as-shipped teapot (teapot.h:77, divs 100: 640,000 triangles)
+    ("s2_d100", lambda: scenes.s2_cornell_teapot(divs=100)[0], 32, 32, 8, 50),
     # sphere and triangle lights next to the rect in the light list
     ("s6_lights", lambda: scenes.s6_mixed_lights()[0], 32, 32, 16, 50),
     # C4 / C5 stand-ins at their configured mesh (divs 40: 102,400 triangles)

@@ -120,6 +120,8 @@ def test_sample_windows_do_not_change_the_frame(monkeypatch):
     (scenes.s2_cornell_teapot, 256, 256, 16),
     (lambda: scenes.s3_cornell_teapot_microfacet("beckmann"), 256, 256, 16),
     (lambda: scenes.s4_soldier_standin(divs=20, fog=True), 192, 108, 8),
+    # the reference's as-shipped teapot (teapot.h:77: 640,000 triangles)
+    (lambda: scenes.s2_cornell_teapot(divs=100), 512, 512, 8),
     # C4 / C5 at their configured frame and mesh (1920x1080, 102,400 triangles)
     (lambda: scenes.s4_soldier_standin(divs=40), 1920, 1080, 4),
     (lambda: scenes.s4_soldier_standin(divs=40, fog=True), 1920, 1080, 2),
