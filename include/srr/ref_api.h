@@ -25,11 +25,22 @@
  * starts at the reference's post-Perlin state (Q14). */
 #pragma once
 
+#include <stdlib.h>  // glibc's drand48 declared before the reference's name is mapped below
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 #include <vector>
 
 #include "../srr_capi.h"
+#include "merl.h"
+
+/* The reference defines its own global drand48() (mathf.h:14-19), which clashes
+ * with glibc's; as in the reference's Linux build (oracle/ref/shim.h), the name is
+ * mapped to the scene-build LCG below. */
+#define drand48 srr_ref_drand48
 
 namespace srr {
 namespace ref {
@@ -64,7 +75,15 @@ inline int check(int h) {
 }
 
 /* mathf.h:14-19 drand48() on the scene-build LCG (bvh_node's random axis uses it) */
-inline double drand48() { return srr_scene_drand48(cur()); }
+inline double srr_ref_drand48() { return srr_scene_drand48(cur()); }
+
+/* stb_image's stbi_load (stb_image.h v2.19) as the builders call it, through srr's
+ * stb-exact decoder (srr_image_load); free with stbi_image_free. */
+inline unsigned char* stbi_load(const char* path, int* x, int* y, int* comp, int req_comp) {
+  unsigned char* p = nullptr;
+  return srr_image_load(path, req_comp, x, y, comp, &p) < 0 ? nullptr : p;
+}
+inline void stbi_image_free(void* p) { srr_image_free((unsigned char*)p); }
 
 /* vec3.h: the value type the builders pass around (float x3) */
 class vec3 {
@@ -83,6 +102,8 @@ class vec3 {
   float operator[](int i) const { return e[i]; }
   float& operator[](int i) { return e[i]; }
   vec3 operator-() const { return vec3(-e[0], -e[1], -e[2]); }
+  float squared_length() const { return e[0] * e[0] + e[1] * e[1] + e[2] * e[2]; }  // vec3.h
+  float length() const { return std::sqrt(e[0] * e[0] + e[1] * e[1] + e[2] * e[2]); }
 };
 inline vec3 operator+(const vec3& a, const vec3& b) { return vec3(a.e[0] + b.e[0], a.e[1] + b.e[1], a.e[2] + b.e[2]); }
 inline vec3 operator-(const vec3& a, const vec3& b) { return vec3(a.e[0] - b.e[0], a.e[1] - b.e[1], a.e[2] - b.e[2]); }
@@ -120,7 +141,10 @@ class material {  // material.h:82-93
   int handle = -1;
   virtual ~material() = default;
 };
-inline int mat_handle(const material* m) { return m ? m->handle : -1; }  // null material*: -1
+inline int mat_handle(const material* m) {  // null material*: -1
+  if (m && m->handle == -2) throw error(SRR_ENOTSUP, "brdfmaterial cannot be rendered (it sets no pdf, SURVEY Q23)");
+  return m ? m->handle : -1;
+}
 class lambertian : public material {  // material.h:95-114
  public:
   lambertian(texture* a) { handle = check(srr_lambertian(cur(), a->handle)); }
@@ -148,6 +172,52 @@ class diffuse_light : public material {  // material.h:341-356
 class isotropic : public material {  // material.h:359-369
  public:
   isotropic(texture* a) { handle = check(srr_isotropic(cur(), a->handle)); }
+};
+
+/* brdf.h's MERL reader (brdf::read_brdf, :156-185; messages as the reference
+ * prints them) and lookup (brdf::lookup_brdf_val, :190-214), on the host.  The
+ * GPU lookup is srr_merl_lookup. */
+class brdf {
+ public:
+  bool read_brdf(const char* filename, double*& table) {
+    FILE* f = std::fopen(filename, "rb");
+    std::printf(f ? "the file was opened\n" : "the file was not opened\n");
+    if (!f) return false;
+    int dims[3] = {0, 0, 0};
+    const bool hdr = std::fread(dims, sizeof(int), 3, f) == 3;
+    const long long n = (long long)dims[0] * dims[1] * dims[2];
+    if (!hdr || n != merl::kCells) {
+      std::fprintf(stderr, "Dimensions don't match\n");
+      std::fclose(f);
+      return false;
+    }
+    table = (double*)std::malloc(sizeof(double) * 3 * n);
+    const size_t got = std::fread(table, sizeof(double), 3 * n, f);
+    std::fclose(f);
+    return got == (size_t)(3 * n);
+  }
+  void lookup_brdf_val(double* table, double theta_in, double fi_in, double theta_out, double fi_out, double& red,
+                       double& green, double& blue) {
+    merl::rgb_of(table, merl::cell_of(theta_in, fi_in, theta_out, fi_out), red, green, blue);
+    if (red < 0.0 || green < 0.0 || blue < 0.0) std::fprintf(stderr, "Below horizon.\n");
+  }
+};
+
+/* material.h:201-241.  The reference reads the table but its scatter() never
+ * sets a pdf, so a hitable carrying one cannot be rendered there:
+ * constructing one works (cornell_box and soldier_scene do, unused); putting it
+ * on a primitive throws. */
+constexpr int kUnrenderableMaterial = -2;
+class brdfmaterial : public material {
+ public:
+  brdfmaterial(const char* brdf_filename, const vec3& a) : albedo(a) {
+    brdf_reader = new brdf();
+    brdf_reader->read_brdf(brdf_filename, brdf_data);
+    handle = kUnrenderableMaterial;
+  }
+  brdf* brdf_reader;
+  double* brdf_data = nullptr;
+  vec3 albedo;
 };
 
 /* ------------------------------------------------------------------ hitables */

@@ -51,6 +51,14 @@ int srr_scene_text_handle(const srr_scene* s, int text_id);
  * mathf.h:12) that the next srr_bvh_node() consumes; default is the
  * post-Perlin state 24561125610955 (perlin.h:94-97). */
 int srr_scene_set_lcg(srr_scene* s, uint64_t state);
+/* FNV-1a-64 digest of the scene's flattened device tables (no GPU needed): two
+ * scenes with equal digests render identically (used to pin scene builders).
+ * parts: NULL or SRR_DIGEST_PARTS per-table digests (objects, n_world,
+ * transforms, spheres, rects, triangles, meshes, BVH2, BVH4, triangle
+ * positions, triangle shading, media, object BVHs, their children, materials,
+ * textures, image bytes, Perlin vectors, Perlin permutations, lights, camera). */
+#define SRR_DIGEST_PARTS 21
+int srr_scene_digest(const srr_scene* s, uint64_t* out, uint64_t* parts);
 uint64_t srr_scene_get_lcg(const srr_scene* s);
 /* drand48() on the scene LCG (mathf.h:14-19), for builders that draw. */
 double srr_scene_drand48(srr_scene* s);
@@ -199,6 +207,25 @@ int srr_accum_set(srr_renderer* r, const float* sums, int64_t npix, int64_t samp
 /* After a render with SRR_FLAG_KEEP_PATHS: per-path raw radiance (before
  * de_nan) and world-ray counts, [n_shard_pixels][spp]. */
 int srr_copy_paths(srr_renderer* r, float* radiance, unsigned char* rays);
+/* ---- MERL measured isotropic BRDF tables (brdf.h).  The reference reads a
+ * table (brdf::read_brdf, brdf.h:156-185) and looks values up by half/difference
+ * angles (brdf::lookup_brdf_val, :190-214); its only user, brdfmaterial
+ * (material.h:201-241), never sets a pdf and is never placed in a scene
+ * (SURVEY Q23), so the lookup is exposed on its own. */
+typedef struct srr_merl srr_merl;
+/* brdf::read_brdf: int32 dims[3], then 3 * dims[0]*dims[1]*dims[2] doubles
+ * (channel-major); the product must be 90*90*180 (else SRR_EINVAL, the
+ * reference's "Dimensions don't match").  Uploads the table to HIP device `device`. */
+int srr_merl_load(const char* path, int device, srr_merl** out);
+/* The same from memory: n_doubles must be 3*90*90*180. */
+int srr_merl_create(const double* table, int64_t n_doubles, int device, srr_merl** out);
+void srr_merl_destroy(srr_merl* m);
+/* brdf::lookup_brdf_val for n queries on the device.  angles: 4n doubles
+ * (theta_in, fi_in, theta_out, fi_out); rgb: 3n doubles out (RED/GREEN/BLUE_SCALE
+ * applied, brdf.h:11-13); cell: n table indices out (may be NULL).  Host buffers.
+ * (The reference's "Below horizon." stderr message is not printed.) */
+int srr_merl_lookup(srr_merl* m, int64_t n, const double* angles, double* rgb, int32_t* cell);
+
 /* Tone map (Raytracing_n.cpp:850-867): 8-bit = clamp(int(255.99*sqrt(m))). */
 int srr_tonemap(const float* mean, int64_t n_pixels, unsigned char* rgb8);
 /* Write an ASCII P3 PPM (Raytracing_n.cpp:886, 873-876). */

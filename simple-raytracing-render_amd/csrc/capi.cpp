@@ -15,6 +15,7 @@
 #include "../../include/srr_capi.h"
 #include "imageio.h"
 #include "meshio.h"
+#include "../../include/srr/merl.h"
 #include "renderer.h"
 
 using namespace srr;
@@ -70,6 +71,62 @@ int srr_scene_text_handle(const srr_scene* s, int id) {
   for (auto& kv : s->s.text_ids)
     if (kv.first == id) return kv.second;
   return fail(SRR_EINVAL, "no such text object id");
+}
+
+// FNV-1a 64 over the flattened device tables (scene.h Flat): two scenes with the
+// same digest upload byte-identical objects, transforms, primitives, BVHs (both
+// layouts), triangles, media, materials, textures and image bytes, lights and camera.
+// parts (optional, SRR_DIGEST_PARTS entries): one digest per table, in that order.
+int srr_scene_digest(const srr_scene* s, uint64_t* out, uint64_t* parts) {
+  if (!s || !out) return fail(SRR_EINVAL, "null argument");
+  Flat f;
+  std::string err;
+  const int rc = flatten(s->s, f, err);
+  if (rc < 0) return fail(rc, err);
+  uint64_t h = 0xcbf29ce484222325ULL;
+  int part = 0;
+  auto mix = [](uint64_t& x, const void* p, size_t n) {
+    const unsigned char* b = (const unsigned char*)p;
+    for (size_t i = 0; i < n; ++i) x = (x ^ b[i]) * 0x100000001b3ULL;
+  };
+  auto blob = [&](const void* p, size_t n) {
+    mix(h, &n, sizeof n);
+    mix(h, p, n);
+    if (const char* dd = getenv("SRR_DIGEST_DUMP")) {  // diagnostics: each table to <prefix>.<part>
+      FILE* df = fopen((std::string(dd) + "." + std::to_string(part)).c_str(), "wb");
+      if (df) { fwrite(p, 1, n, df); fclose(df); }
+    }
+    if (parts) {
+      uint64_t x = 0xcbf29ce484222325ULL;
+      mix(x, p, n);
+      parts[part] = x;
+    }
+    ++part;
+  };
+  auto vec = [&blob](const auto& v) { blob(v.data(), v.size() * sizeof(v[0])); };
+  vec(f.objs);
+  blob(&f.n_world, sizeof f.n_world);
+  vec(f.xforms);
+  vec(f.spheres);
+  vec(f.rects);
+  vec(f.stris);
+  vec(f.meshes);
+  vec(f.nodes);
+  vec(f.node4);
+  vec(f.tri_pos);
+  vec(f.tri_shade);
+  vec(f.media);
+  vec(f.obvhs);
+  vec(f.obvh_children);
+  vec(f.mats);
+  vec(f.texs);
+  vec(f.images);
+  vec(f.perlin_ranvec);
+  vec(f.perlin_perm);
+  vec(f.lights);
+  blob(&f.cam, sizeof f.cam);
+  *out = h;
+  return 0;
 }
 
 int srr_scene_set_lcg(srr_scene* s, uint64_t state) {
@@ -592,6 +649,76 @@ int srr_device_kat(const char* name, int n, int width, float* records) {
   for (void* p : {(void*)d_rec, (void*)d_aux, (void*)d_tris, (void*)d_cams, (void*)d_rects, (void*)d_sph,
                   (void*)d_stris, (void*)d_lights})
     (void)hipFree(p);
+  return rc;
+}
+
+// ---- MERL tables (brdf.h)
+struct srr_merl {
+  int device = 0;
+  double* table = nullptr;  // device: 3 * merl::kCells doubles
+};
+
+int srr_merl_create(const double* table, int64_t n_doubles, int device, srr_merl** out) {
+  if (!table || !out) return fail(SRR_EINVAL, "null argument");
+  if (n_doubles != 3 * (int64_t)merl::kCells) return fail(SRR_EINVAL, "MERL table: dimensions don't match");
+  HIPCHK(hipSetDevice(device));
+  auto m = std::make_unique<srr_merl>();
+  m->device = device;
+  HIPCHK(hipMalloc((void**)&m->table, (size_t)n_doubles * sizeof(double)));
+  if (hipMemcpy(m->table, table, (size_t)n_doubles * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(m->table);
+    return fail(SRR_EIO, "MERL table upload failed");
+  }
+  *out = m.release();
+  return 0;
+}
+
+int srr_merl_load(const char* path, int device, srr_merl** out) {  // brdf::read_brdf (brdf.h:156-185)
+  if (!path || !out) return fail(SRR_EINVAL, "null argument");
+  FILE* f = fopen(path, "rb");
+  if (!f) return fail(SRR_EIO, std::string("cannot open MERL table ") + path);
+  int32_t dims[3] = {0, 0, 0};
+  const bool hdr = fread(dims, sizeof(int32_t), 3, f) == 3;
+  const int64_t n = (int64_t)dims[0] * dims[1] * dims[2];
+  if (!hdr || n != merl::kCells) {
+    fclose(f);
+    return fail(SRR_EINVAL, "MERL table: dimensions don't match");
+  }
+  std::vector<double> t(3 * (size_t)n);
+  const size_t got = fread(t.data(), sizeof(double), t.size(), f);
+  fclose(f);
+  if (got != t.size()) return fail(SRR_EINVAL, "MERL table: truncated file");
+  return srr_merl_create(t.data(), (int64_t)t.size(), device, out);
+}
+
+void srr_merl_destroy(srr_merl* m) {
+  if (!m) return;
+  (void)hipSetDevice(m->device);
+  (void)hipFree(m->table);
+  delete m;
+}
+
+int srr_merl_lookup(srr_merl* m, int64_t n, const double* angles, double* rgb, int32_t* cell) {
+  if (!m || n < 0 || (n > 0 && (!angles || !rgb))) return fail(SRR_EINVAL, "bad MERL lookup arguments");
+  if (n == 0) return 0;
+  HIPCHK(hipSetDevice(m->device));
+  double *d_ang = nullptr, *d_rgb = nullptr;
+  int32_t* d_cell = nullptr;
+  int rc = 0;
+  if (hipMalloc((void**)&d_ang, 4 * (size_t)n * sizeof(double)) != hipSuccess ||
+      hipMalloc((void**)&d_rgb, 3 * (size_t)n * sizeof(double)) != hipSuccess ||
+      (cell && hipMalloc((void**)&d_cell, (size_t)n * sizeof(int32_t)) != hipSuccess))
+    rc = fail(SRR_ENOMEM, "device allocation failed");
+  if (!rc && hipMemcpy(d_ang, angles, 4 * (size_t)n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess)
+    rc = fail(SRR_EIO, "copy to device failed");
+  if (!rc && launch_merl_lookup(m->table, n, d_ang, d_rgb, d_cell) < 0) rc = fail(SRR_EIO, "MERL kernel launch failed");
+  if (!rc && (hipDeviceSynchronize() != hipSuccess ||
+              hipMemcpy(rgb, d_rgb, 3 * (size_t)n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess ||
+              (cell && hipMemcpy(cell, d_cell, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess)))
+    rc = fail(SRR_EIO, "MERL kernel failed");
+  (void)hipFree(d_ang);
+  (void)hipFree(d_rgb);
+  (void)hipFree(d_cell);
   return rc;
 }
 

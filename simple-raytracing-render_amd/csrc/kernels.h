@@ -117,6 +117,8 @@ struct KatTables {
 };
 int launch_kat(int kind, int n, int w, float* d_rec, const float* d_aux, const DStandaloneTri* d_tris,
                const KatTables& kt);
+// MERL table lookup (merl.h) for n queries; device pointers
+int launch_merl_lookup(const double* table, int64_t n, const double* angles, double* rgb, int32_t* cell);
 void launch_accumulate_window(const float* sample, int npix, int spp_w, float* acc, hipStream_t st);
 void launch_raygen(const SceneView& S, const PathState& P, const BatchInfo& B, hipStream_t st);
 void launch_trace(const SceneView& S, const PathState& P, const int* active, const int* count, int max_n,

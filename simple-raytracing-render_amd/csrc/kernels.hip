@@ -21,6 +21,7 @@
 #include "device_scene.h"
 #include "devmath.h"
 #include "kernels.h"
+#include "../../include/srr/merl.h"
 
 namespace srr {
 namespace dev {
@@ -2153,6 +2154,23 @@ __global__ void k_finish(const float* acc, float* mean, int64_t n, int ns) {
   mean[i] = acc[i] * k;
 }
 
+// ------------------------------------------------------------ MERL lookup
+// brdf::lookup_brdf_val (brdf.h:190-214) for n direction pairs: one query per
+// thread, angles[4q..4q+3] = (theta_in, fi_in, theta_out, fi_out).
+__global__ void __launch_bounds__(256) k_merl_lookup(const double* table, int64_t n, const double* angles,
+                                                     double* rgb, int32_t* cell) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= n) return;
+  const double* a = angles + 4 * q;
+  const int c = merl::cell_of(a[0], a[1], a[2], a[3]);
+  double r, g, b;
+  merl::rgb_of(table, c, r, g, b);
+  rgb[3 * q] = r;
+  rgb[3 * q + 1] = g;
+  rgb[3 * q + 2] = b;
+  if (cell) cell[q] = c;
+}
+
 // ------------------------------------------------- device known-answer tests
 // Test infrastructure (srr_device_kat): the product's device functions on the
 // reference's KAT records (tests/golden/kat_*.bin, layouts in oracle/ref/kat.inc):
@@ -2522,6 +2540,13 @@ void launch_paths(const SceneView& S, const PathWork& W, int all_families, hipSt
   }
 #undef SRR_LAUNCH_PATHS_B
 #undef SRR_LAUNCH_PATHS
+}
+
+int launch_merl_lookup(const double* table, int64_t n, const double* angles, double* rgb, int32_t* cell) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(dev::k_merl_lookup, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, table, n, angles, rgb,
+                     cell);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
 int launch_kat(int kind, int n, int w, float* d_rec, const float* d_aux, const DStandaloneTri* d_tris,

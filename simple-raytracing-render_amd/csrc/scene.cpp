@@ -959,6 +959,77 @@ struct Flattener {
 };
 }  // namespace
 
+// Keeps only the materials the flattened objects reference and the textures
+// (and image bytes) those materials reach, in their construction order.  The
+// reference's builders construct materials they never place (cornell_box makes
+// 20, uses 4); dropping them changes no lookup, shrinks the LDS-staged world
+// tables, lets the diffuse-only kernel variant run when only diffuse materials
+// are placed, and makes two builds of one scene flatten to identical tables
+// whatever unused materials either constructed (srr_scene_digest).
+static void compact_materials(Flat& F) {
+  const int nm = (int)F.mats.size(), nt = (int)F.texs.size();
+  std::vector<int> mmap(nm, -1), tmap(nt, -1);
+  auto use_mat = [&](int m) {
+    if (m >= 0 && m < nm) mmap[m] = 0;
+  };
+  for (const DSphere& x : F.spheres) use_mat(x.mat);
+  for (const DRect& x : F.rects) use_mat(x.mat);
+  for (const DStandaloneTri& x : F.stris) use_mat(x.sh.mat);
+  for (const TriShade& x : F.tri_shade) use_mat(x.mat);
+  for (const DMedium& x : F.media) use_mat(x.phase_mat);
+  std::vector<int> stack;
+  for (int m = 0; m < nm; ++m)
+    if (mmap[m] == 0 && F.mats[m].tex >= 0) stack.push_back(F.mats[m].tex);
+  while (!stack.empty()) {  // textures reached, through checker children
+    const int t = stack.back();
+    stack.pop_back();
+    if (t < 0 || t >= nt || tmap[t] == 0) continue;
+    tmap[t] = 0;
+    if (F.texs[t].kind == TEX_CHECKER) {
+      stack.push_back(F.texs[t].even);
+      stack.push_back(F.texs[t].odd);
+    }
+  }
+  std::vector<DTex> texs;
+  std::vector<uint8_t> images;
+  for (int t = 0; t < nt; ++t) {
+    if (tmap[t] < 0) continue;
+    tmap[t] = (int)texs.size();
+    DTex d = F.texs[t];
+    if (d.kind == TEX_IMAGE) {
+      const size_t bytes = 3 * (size_t)d.nx * d.ny;
+      const int64_t off = (int64_t)images.size();
+      images.insert(images.end(), F.images.begin() + d.off, F.images.begin() + d.off + bytes);
+      d.off = off;
+    }
+    texs.push_back(d);
+  }
+  for (DTex& d : texs)
+    if (d.kind == TEX_CHECKER) {
+      d.even = tmap[d.even];
+      d.odd = tmap[d.odd];
+    }
+  std::vector<DMat> mats;
+  for (int m = 0; m < nm; ++m) {
+    if (mmap[m] < 0) continue;
+    mmap[m] = (int)mats.size();
+    DMat d = F.mats[m];
+    if (d.tex >= 0) d.tex = tmap[d.tex];
+    mats.push_back(d);
+  }
+  auto remap = [&](int32_t& m) {
+    if (m >= 0 && m < nm) m = mmap[m];
+  };
+  for (DSphere& x : F.spheres) remap(x.mat);
+  for (DRect& x : F.rects) remap(x.mat);
+  for (DStandaloneTri& x : F.stris) remap(x.sh.mat);
+  for (TriShade& x : F.tri_shade) remap(x.mat);
+  for (DMedium& x : F.media) remap(x.phase_mat);
+  F.mats = std::move(mats);
+  F.texs = std::move(texs);
+  F.images = std::move(images);
+}
+
 int flatten(const Scene& S, Flat& F, std::string& err) {
   F = Flat();
   if (S.world < 0 || S.lights < 0 || !S.has_camera) {
@@ -1007,6 +1078,7 @@ int flatten(const Scene& S, Flat& F, std::string& err) {
     }
     F.lights.push_back(fl.light(k));
   }
+  compact_materials(F);
   perlin_tables(F.perlin_ranvec, F.perlin_perm);
   const HCamera& c = S.cam;
   std::memcpy(F.cam.origin, c.origin, 12);

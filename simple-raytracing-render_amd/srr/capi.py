@@ -58,6 +58,10 @@ def lib():
         L.srr_shard_pixels.restype = ctypes.c_int64
         L.srr_shard_pixels.argtypes = [ctypes.POINTER(Params), vp]
         L.srr_render_device.argtypes = [vp, ctypes.POINTER(Params), vp, ctypes.POINTER(Stats)]
+        L.srr_merl_load.argtypes = [cp, ip, ctypes.POINTER(vp)]
+        L.srr_merl_create.argtypes = [vp, ctypes.c_int64, ip, ctypes.POINTER(vp)]
+        L.srr_merl_destroy.argtypes = [vp]
+        L.srr_merl_lookup.argtypes = [vp, ctypes.c_int64, vp, vp, vp]
         L.srr_render.argtypes = [vp, ctypes.POINTER(Params), vp, vp, ctypes.POINTER(Stats)]
         L.srr_copy_paths.argtypes = [vp, vp, vp]
         L.srr_tonemap.argtypes = [vp, ctypes.c_int64, vp]
@@ -117,6 +121,43 @@ class Scene:
     def __del__(self):
         if getattr(self, "h", None):
             lib().srr_scene_destroy(self.h)
+            self.h = None
+
+
+MERL_CELLS = 90 * 90 * 180  # doubles per channel of a MERL table (brdf.h:7-9)
+
+
+class Merl:
+    """A MERL measured-BRDF table on the GPU: the reference's ``brdf`` class
+    (brdf.h).  ``Merl.load(path)`` is brdf::read_brdf, ``Merl(table)`` takes the
+    3 * 90*90*180 doubles directly, ``lookup`` is brdf::lookup_brdf_val for a
+    batch of (theta_in, fi_in, theta_out, fi_out) rows."""
+
+    def __init__(self, table=None, device: int = 0, _handle=None):
+        self.h = _handle
+        if self.h is None:
+            t = np.ascontiguousarray(table, dtype=np.float64).ravel()
+            h = ctypes.c_void_p()
+            _check(lib().srr_merl_create(t.ctypes.data, t.size, device, ctypes.byref(h)))
+            self.h = h
+
+    @classmethod
+    def load(cls, path: str, device: int = 0) -> "Merl":
+        h = ctypes.c_void_p()
+        _check(lib().srr_merl_load(path.encode(), device, ctypes.byref(h)))
+        return cls(_handle=h)
+
+    def lookup(self, angles) -> tuple[np.ndarray, np.ndarray]:
+        """angles: [n, 4] (theta_in, fi_in, theta_out, fi_out) -> (rgb [n, 3] f64, cell [n] int32)."""
+        a = np.ascontiguousarray(angles, dtype=np.float64).reshape(-1, 4)
+        rgb = np.zeros((a.shape[0], 3), np.float64)
+        cell = np.zeros(a.shape[0], np.int32)
+        _check(lib().srr_merl_lookup(self.h, a.shape[0], a.ctypes.data, rgb.ctypes.data, cell.ctypes.data))
+        return rgb, cell
+
+    def __del__(self):
+        if getattr(self, "h", None) and _LIB is not None:
+            _LIB.srr_merl_destroy(self.h)
             self.h = None
 
 

@@ -37,6 +37,11 @@ def _f32(x):
     return np.float32(x)
 
 
+def _size_t_f32(x: int) -> float:
+    """An unsigned 64-bit (size_t) expression converted to float, as C++ does."""
+    return float(np.float32(float(x % (1 << 64))))
+
+
 def _asset(contents, *parts):
     return os.path.join(contents or CONTENTS, *parts)
 
@@ -167,7 +172,9 @@ def ball_scenes(aspect: float, contents: str | None = None) -> Scene:
     ]
     for j in range(121):
         m = sc.beckmann(sc.constant_texture(1), float(_f32(j % 11) / _f32(11)), float(_f32(j // 11) / _f32(11)))
-        objs.append(sc.sphere((550 - (j % 11) * 50, 20, 450 - 50 * (j // 11)), 20, m))
+        # j is a size_t (Raytracing_n.cpp:400): 450 - 50*(j/11) wraps for the last
+        # row (j >= 110) to 2^64 - 50, which the vec3 float rounds to 2^64
+        objs.append(sc.sphere((_size_t_f32(550 - (j % 11) * 50), 20, _size_t_f32(450 - 50 * (j // 11))), 20, m))
     sc.set_world(sc.hitable_list(objs))
     sc.set_lights(sc.hitable_list([sc.flip_normals(sc.xz_rect(203, 353, 217, 343, 800))]))
     return sc

@@ -153,3 +153,20 @@ def test_gpu_reference_builders(standin, name):
     assert pc["match"] >= parity.MIN_MATCH, (name, pc)
     assert pc["bitexact"] >= parity.MIN_BITEXACT, (name, pc)
     assert int(out["stats"]["world_rays"]) == int(ref["stats"][0])
+
+
+@pytest.mark.gpu
+def test_render_main_writes_the_reference_ppm(standin, tmp_path):
+    """srr.render_main, the reference's main() (Raytracing_n.cpp:882-952): sceneid
+    -> builder -> GPU render -> P3 PPM, byte-equal to tone-mapping the same
+    render by hand."""
+    from srr import capi, render_main
+    out = str(tmp_path / "main.ppm")
+    assert render_main.main(["--sceneid", "5", "--nx", "24", "--ny", "18", "--ns", "4", "--contents", standin,
+                             "--out", out]) == 0
+    sc = ref_scenes.BY_SCENEID[5](24 / 18, standin)
+    img8 = capi.tonemap(capi.Renderer(sc.text()).render(24, 18, 4, 50)["mean"])
+    want = str(tmp_path / "want.ppm")
+    capi.write_ppm(want, 24, 18, img8)
+    assert open(out, "rb").read() == open(want, "rb").read()
+    assert open(out, "rb").read().startswith(b"P3\n24 18\n255\n")
