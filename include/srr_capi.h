@@ -180,6 +180,8 @@ typedef struct srr_stats {
   int64_t tri_tests;    /*   triangle tests (a 1-triangle leaf counts 2, as    */
                         /*   the reference tests it twice, bvh.h:104-105)      */
   int64_t stack_overflows; /* rays re-walked on the stackless BVH2             */
+  int64_t deep_traversals; /* path engine: mesh traversals whose stack went past */
+                           /* its LDS part into the global extension           */
 } srr_stats;
 
 /* Flatten the scene and upload it to HIP device `device`. */

@@ -97,7 +97,10 @@ struct PathWork {
   int lanes;              // persistent lanes (grid * block)
   int* err;               // guard bits set on an out-of-range index (never expected)
   int stack_cap;          // BVH4 traversal stack entries (kStack = 8; fewer forces the exact re-walk)
+  int2* gstack;           // the stack's global extension [gstack_cap][lanes] (deep meshes), or nullptr
+  int gstack_cap;
 };
+constexpr int kPathsGlobalStack = 56;  // global stack entries per lane beyond the LDS ones
 
 constexpr int kPathsWorldLdsBytes = 8192;  // == kernels.hip kWorldLdsBytes
 constexpr int kPathsLdsNodes = 96;         // BVH4 nodes cached in LDS by k_paths (12 KB)

@@ -220,6 +220,13 @@ struct TraceCtx {
   int lds_count = 0;
   int st_cap = kStack;                   // stack entries used (<= kStack; SRR_STACK_CAP tests the re-walk)
   unsigned long long* ovf = nullptr;     // optional: += 1 per traversal that overflowed into the re-walk
+  // optional global extension of the stack (k_paths): entries kStack.. of lane
+  // `slot` at gst[(sp - st_cap) * gst_stride + slot] = (node, entry t bits), up to
+  // gst_cap of them; only a traversal deeper than that re-walks the BVH2
+  int2* gst = nullptr;
+  int gst_cap = 0;
+  int gst_stride = 0;
+  int slot = 0;
   // SRR_TIMING diagnostics (wave-uniform): cycles inside mesh traversals, steps
   mutable uint64_t mesh_cycles = 0;
   mutable int mesh_steps = 0;
@@ -254,7 +261,7 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
   float bound = tmax;
   int node = m.node4_off;
   int sp = 0;
-  bool overflow = false;
+  bool overflow = false, deep = false;
   uint32_t nbox = 0, ntri = 0;
   const uint64_t tm_enter = TIMING ? __builtin_amdgcn_s_memtime() : 0;
   for (;;) {
@@ -345,6 +352,10 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
           cx.st_node[sp * kTraceBlock] = kn[c];
           cx.st_t[sp * kTraceBlock] = kt[c];
           ++sp;
+        } else if (sp < cx.st_cap + cx.gst_cap) {
+          cx.gst[(size_t)(sp - cx.st_cap) * cx.gst_stride + cx.slot] = make_int2(kn[c], __float_as_int(kt[c]));
+          ++sp;
+          deep = true;
         } else {
           overflow = true;
         }
@@ -355,8 +366,17 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
     int nx = -1;
     while (sp > 0) {
       --sp;
-      const int cand = cx.st_node[sp * kTraceBlock];
-      if (!(PRUNE && cx.st_t[sp * kTraceBlock] > bound)) { nx = cand; break; }
+      int cand;
+      float ct;
+      if (sp < cx.st_cap) {
+        cand = cx.st_node[sp * kTraceBlock];
+        ct = cx.st_t[sp * kTraceBlock];
+      } else {
+        const int2 e = cx.gst[(size_t)(sp - cx.st_cap) * cx.gst_stride + cx.slot];
+        cand = e.x;
+        ct = __int_as_float(e.y);
+      }
+      if (!(PRUNE && ct > bound)) { nx = cand; break; }
     }
     if (nx < 0) break;
     node = nx;
@@ -377,6 +397,10 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
     for (int o = 32; o > 0; o >>= 1) st = max(st, __shfl_xor(st, o));
     cx.mesh_steps += st;
     cx.mesh_cycles += __builtin_amdgcn_s_memtime() - tm_enter;
+  }
+  if (cx.ovf && cx.gst) {  // traversals that used the global stack (one atomic per wave)
+    const uint64_t dm = __ballot(deep);
+    if (dm && (int)__lane_id() == __ffsll((unsigned long long)dm) - 1) atomicAdd(cx.ovf + 1, (unsigned long long)__popcll(dm));
   }
   if (overflow) {  // rare: exact re-walk
     if (cx.ovf) atomicAdd(cx.ovf, 1ull);
@@ -1319,8 +1343,9 @@ constexpr int kMaxHelpers = SRR_COOP_HELPERS;  // attempts of one path per round
 // Out: ndir, pdf and the LCG state after the first attempt with pdf != 0 (or the
 // guard's last attempt).  The first round is each pending lane's own attempt
 // (no exchange); later rounds spread the remaining paths over all 64 lanes.
-SRR_D void coop_mixture(const SceneView& S, const DiffSetup& me, bool& pend, int& tries, uint64_t& lcg, V3& ndir,
-                        float& pdf) {
+SRR_D int coop_mixture(const SceneView& S, const DiffSetup& me, bool& pend, int& tries, uint64_t& lcg, V3& ndir,
+                       float& pdf) {
+  int rounds = 0;
   const int lane = lane_id();
   const uint64_t lt = (1ull << lane) - 1;
   uint64_t F = __ballot(pend);
@@ -1402,7 +1427,9 @@ SRR_D void coop_mixture(const SceneView& S, const DiffSetup& me, bool& pend, int
       }
     }
     F = __ballot(pend);
+    ++rounds;
   }
+  return rounds;
 }
 
 // camera::get_ray(s, t) (camera.h:51-59; random_in_unit_disk camera.h:8-14)
@@ -1792,7 +1819,7 @@ constexpr unsigned long long kPoolChunk = 64;  // path indices a wave takes per 
 template <bool MEDIA, bool ALLFAM, int MINB, bool TIMED = false, bool WL = true>
 __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathWork W) {
   // TIMED (diagnostics): per-wave cycles in refill / world hit (mesh part) / record+scatter / fold
-  uint64_t tp[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t tp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t it = 0;
   SceneView S = S0;
   // WL: world tables staged in LDS (they fit in kWorldLdsBytes); otherwise read
@@ -1824,7 +1851,11 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
   cx.lds_count = S0.node4_lds;
   cx.st_cap = W.stack_cap;
   cx.ovf = W.counters + 11;
+  cx.gst = W.gstack;
+  cx.gst_cap = W.gstack ? W.gstack_cap : 0;
+  cx.gst_stride = W.lanes;
   const int slot = blockIdx.x * blockDim.x + threadIdx.x;
+  cx.slot = slot;
   int g = -1;  // path of this lane (a window numbers its paths below 2^31), -1 idle
   const uint32_t n_paths = (uint32_t)W.n_paths;
   // the wave's unissued path indices [pool, pool_end): wave-uniform (scalar)
@@ -1954,7 +1985,14 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
         }
       }
     }
-    if (__ballot(pend)) coop_mixture(S, ds, pend, d_tries, rng.lcg, d_dir, d_pdf);
+    if (__ballot(pend)) {
+      const uint64_t tc = TIMED ? __builtin_amdgcn_s_memtime() : 0;
+      const int rounds = coop_mixture(S, ds, pend, d_tries, rng.lcg, d_dir, d_pdf);
+      if (TIMED) {
+        tp[6] += __builtin_amdgcn_s_memtime() - tc;
+        tp[7] += rounds;
+      }
+    }
     if (diff) {  // the rest of scatter<FAM_DIFF>: scattering_pdf and the record
       float c = dot(d_n, unit_vector(d_dir));  // material.h:100-105, 134-138
       if (c < 0) c = 0;
@@ -2006,6 +2044,8 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
     for (int q = 0; q < 5; ++q) atomicAdd(W.counters + 4 + q, (unsigned long long)tp[q]);
     atomicAdd(W.counters + 9, (unsigned long long)it);
     atomicAdd(W.counters + 10, (unsigned long long)tp[5]);
+    atomicAdd(W.counters + 13, (unsigned long long)tp[6]);
+    atomicAdd(W.counters + 14, (unsigned long long)tp[7]);
   }
   unsigned long long tot = nrays;
   for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);

@@ -115,6 +115,7 @@ int renderer_create(const Scene& sc, int device, srr_renderer** out, std::string
   V.lights = li;
   V.n_lights = (int)F.lights.size();
   V.cam = cm;
+  r->has_meshes = !F.meshes.empty() || !F.obvhs.empty();
   r->diffuse_only = true;
   for (const DMat& m : F.mats)
     if (m.kind != MAT_LAMBERTIAN && m.kind != MAT_ORENNAYAR && m.kind != MAT_DIFFUSE_LIGHT) r->diffuse_only = false;
@@ -285,6 +286,11 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
     RCHK(hipMalloc((void**)&r->pw_rec, rec_need * sizeof(float4)));
     r->pw_rec_cap = rec_need;
   }
+  // global extension of the BVH4 traversal stack, for meshes deep enough to need it
+  // (SRR_GSTACK=0 disables it: every deeper traversal then re-walks the BVH2)
+  const char* gs_env = getenv("SRR_GSTACK");
+  const int gst_cap = (r->has_meshes && !(gs_env && !atoi(gs_env))) ? kPathsGlobalStack : 0;
+  if (gst_cap && !r->pw_gstack) RCHK(hipMalloc((void**)&r->pw_gstack, (size_t)gst_cap * r->pw_lanes * sizeof(int2)));
   // sample window: all pixels x W samples, buffer within SRR_WINDOW_MB (default 8192)
   size_t budget = (size_t)8192 << 20;
   if (const char* e = getenv("SRR_WINDOW_MB")) budget = (size_t)std::max(1, atoi(e)) << 20;
@@ -341,6 +347,8 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
     w.lanes = (int)std::min<int64_t>(r->pw_lanes, ((w.n_paths + 255) / 256) * 256);
     w.stack_cap = 8;  // kernels.hip kStack
     if (const char* e = getenv("SRR_STACK_CAP")) w.stack_cap = std::max(1, std::min(8, atoi(e)));
+    w.gstack = gst_cap ? r->pw_gstack : nullptr;
+    w.gstack_cap = gst_cap;
     RCHK(hipMemsetAsync(w.cursor, 0, sizeof(unsigned long long), st));
     RCHK(hipEventRecord(r->lanes[0].ev_t0, st));
     launch_paths(r->view, w, all_fam ? 1 : 0, st);
@@ -366,6 +374,7 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
     const double it = (double)ctr[9];
     fprintf(stderr, "k_paths per wave-iteration (ticks): refill %.0f  world %.0f  mesh %.0f  record %.0f  scatter %.0f  fold %.0f  (%llu wave-iterations)\n",
             ctr[4] / it, ctr[5] / it, ctr[6] / it, ctr[10] / it, (ctr[7] - ctr[10]) / it, ctr[8] / it, ctr[9]);
+    fprintf(stderr, "  scatter: mixture loop %.0f ticks, %.2f rounds per wave-iteration\n", ctr[13] / it, ctr[14] / it);
   }
   const unsigned long long rays = ctr[0];
   if (ctr[2]) {
@@ -378,6 +387,7 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
   RCHK(hipEventElapsedTime(&total, r->ev_beg, r->ev_end));
   s.world_rays = (int64_t)rays;
   s.stack_overflows = (int64_t)ctr[11];
+  s.deep_traversals = (int64_t)ctr[12];
   s.paths = npix * p->spp;
   s.trace_ms = kernel_ms;
   s.total_ms = total;
@@ -652,6 +662,7 @@ srr_renderer::~srr_renderer() {
   for (void* p : scene_bufs) (void)hipFree(p);
   if (visits) (void)hipFree(visits);
   (void)hipFree(pw_rec);
+  (void)hipFree(pw_gstack);
   (void)hipFree(pw_sample);
   (void)hipFree(pw_raw);
   (void)hipFree(pw_rays);

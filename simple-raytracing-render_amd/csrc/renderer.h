@@ -69,6 +69,8 @@ struct srr_renderer {
   bool diffuse_only = false;  // no beckmann / specular materials: lean kernel variant
   float4* pw_rec = nullptr;
   size_t pw_rec_cap = 0;
+  int2* pw_gstack = nullptr;  // [kPathsGlobalStack][pw_lanes] (kernels.h)
+  bool has_meshes = false;
   float* pw_sample = nullptr;
   float* pw_raw = nullptr;
   uint8_t* pw_rays = nullptr;

@@ -216,19 +216,27 @@ def test_model_file_scene_matches_oracle(tmp_path):
     assert pc["bitexact"] >= parity.MIN_BITEXACT, pc
 
 
-@pytest.mark.parametrize("name", ["s4_d40", "s5_d40"])
-def test_stack_overflow_rewalk_matches_reference(name, monkeypatch):
-    """The BVH4 traversal's LDS stack holds kStack = 8 entries; a ray that needs
-    more re-walks the mesh with the exact stackless BVH2 (kernels.hip mesh_hit4).
-    SRR_STACK_CAP=1 (read per render call) forces that re-walk on most mesh
-    rays of the 102,400-triangle C4/C5 goldens: still every path bit-identical to
-    the reference, and the overflow counter shows the re-walk really ran."""
+@pytest.mark.parametrize("gstack", ["0", "1"])
+@pytest.mark.parametrize("name", ["s4_d40", "s5_d40", "s2_d100"])
+def test_stack_overflow_rewalk_matches_reference(name, gstack, monkeypatch):
+    """The BVH4 traversal's LDS stack holds kStack = 8 entries, extended in global
+    memory by kPathsGlobalStack more; a ray that needs more re-walks the mesh with
+    the exact stackless BVH2 (kernels.hip mesh_hit4).  SRR_STACK_CAP=1 (read per
+    render call) sends most mesh rays of the 102,400- and 640,000-triangle goldens
+    through the global extension (SRR_GSTACK=1) or, without it (SRR_GSTACK=0),
+    through the re-walk: every path still bit-identical to the reference, and the
+    counters show that path really ran."""
     m, text, gp, gr, gi = golden(name)
     monkeypatch.setenv("SRR_STACK_CAP", "1")
+    monkeypatch.setenv("SRR_GSTACK", gstack)
     out = capi.Renderer(text).render(m["nx"], m["ny"], m["spp"], m["max_depth"], keep_paths=True)
     pc = parity.compare_paths(out["paths"], gp)
-    print(name, pc, "overflows:", out["stats"]["stack_overflows"])
-    assert out["stats"]["stack_overflows"] > 0
+    st = out["stats"]
+    print(name, pc, "overflows:", st["stack_overflows"], "deep:", st["deep_traversals"])
+    if gstack == "1":
+        assert st["deep_traversals"] > 0
+    else:
+        assert st["stack_overflows"] > 0 and st["deep_traversals"] == 0
     assert pc["bitexact"] >= parity.MIN_BITEXACT, pc
     assert (out["rays"] == gr).all()
     assert out["stats"]["world_rays"] == m["world_rays"]
