@@ -1451,6 +1451,110 @@ SRR_D void camera_get_ray(const DCamera& C, float u, float v, Rng& rng, V3& o, V
   o = org + offset;
 }
 
+// ------------------------------------------- mixture loop with dead BSDF draws
+// For most diffuse bounces no BSDF-branch sample of the mixture can have a
+// non-zero pdf: the BSDF value of a cosine / Oren-Nayar sample is 0 (SURVEY Q1:
+// the sample is put in the hemisphere opposite the viewer), and every light lies
+// wholly on the far side of the tangent plane from that hemisphere, so the light
+// pdf of the sample is 0 too.  bsdf_dead() proves this per bounce (with margins
+// far above float rounding); the loop then passes over such attempts by their
+// LCG draws alone -- the branch draw, and r1, r2 of random_cosine_direction,
+// whose r2 <= 0.999 keeps the sample's w component >= 0.03, well clear of the
+// tangent plane -- and evaluates exactly only light-branch attempts, near-tangent
+// BSDF samples, and the guard's last attempt.  The attempts it evaluates and
+// their results are the sequential loop's, bit for bit.
+#ifndef SRR_MIXTURE_SKIP
+#define SRR_MIXTURE_SKIP 2
+#endif
+
+SRR_D bool light_point_far(V3 c, V3 p, V3 w, float sgn, float m) { return sgn * dot(c - p, w) <= -m; }
+
+SRR_D bool bsdf_dead(const SceneView& S, const Bsdf& f, V3 p) {
+  // the BSDF value: lambertian |ci|/pi only when ci*co < 0, with sign(ci) the
+  // sample's hemisphere (-1 flipped, +1 not); orennayar's cosine clamps a
+  // flipped sample to 0
+  if (f.kind == MAT_LAMBERTIAN) {
+    if (f.flip ? !(f.co <= 0) : !(f.co >= 0)) return false;
+  } else if (!f.flip) {
+    return false;
+  }
+  const float sgn = f.flip ? -1.f : 1.f;
+  const V3 w = f.uvw.w;
+  const float ps = fmaxf(fmaxf(fabsf(p.x), fabsf(p.y)), fabsf(p.z)) + 1.f;
+  for (int k = 0; k < S.n_lights; ++k) {
+    const DLight L = S.lights[k];
+    if (L.kind == LIGHT_XZRECT) {
+      const DRect q = S.rects[L.idx];
+      if (!(q.k != p[q.kax])) return false;  // the hit point in the light's plane
+      const float m = 1e-3f * (ps + fmaxf(fmaxf(fmaxf(fabsf(q.lo0), fabsf(q.hi0)), fmaxf(fabsf(q.lo1), fabsf(q.hi1))),
+                                          fabsf(q.k)));
+      for (int c = 0; c < 4; ++c) {
+        V3 v = v3(0.f);
+        v.set(q.kax, q.k);
+        v.set(q.a0, (c & 1) ? q.hi0 : q.lo0);
+        v.set(q.a1, (c & 2) ? q.hi1 : q.lo1);
+        if (!light_point_far(v, p, w, sgn, m)) return false;
+      }
+    } else if (L.kind == LIGHT_SPHERE) {
+      const DSphere sp = S.spheres[L.idx];
+      const V3 c = v3(sp.c0[0], sp.c0[1], sp.c0[2]);
+      const float r = fabsf(sp.r);
+      const float m = 1e-3f * (ps + fmaxf(fmaxf(fabsf(c.x), fabsf(c.y)), fabsf(c.z)) + r);
+      if (!light_point_far(c, p, w, sgn, r + m)) return false;
+    } else if (L.kind == LIGHT_TRI) {
+      const DStandaloneTri T = S.stris[L.idx];
+      float cs = 0;
+      for (int k2 = 0; k2 < 9; ++k2) cs = fmaxf(cs, fabsf(T.p[k2]));
+      const float m = 1e-3f * (ps + cs);
+      for (int c = 0; c < 3; ++c)
+        if (!light_point_far(v3(T.p[3 * c], T.p[3 * c + 1], T.p[3 * c + 2]), p, w, sgn, m)) return false;
+    } else if (L.kind != LIGHT_NONE) {
+      return false;
+    }
+  }
+  return true;
+}
+
+// Runs to completion the loops of every lane with `pend`, each on its own path:
+// pass over dead BSDF attempts, evaluate the next candidate attempt exactly,
+// repeat while it fails.  In: the lane's setup and its LCG state before attempt
+// `tries`.  Out: ndir, pdf and the LCG state after the first attempt with
+// pdf != 0 (or the guard's last attempt).  Returns the wave's exact rounds.
+SRR_D int skip_mixture(const SceneView& S, const DiffSetup& me, bool dead, bool& pend, int& tries, uint64_t& lcg,
+                       V3& ndir, float& pdf, int max_rounds = 1 << 30) {
+  int rounds = 0;
+  while (rounds < max_rounds && __ballot(pend)) {
+    if (pend) {
+      uint64_t s = lcg;
+      int t = tries;
+      if (dead) {
+        while (t + 1 < kMixtureGuard) {
+          const uint64_t s1 = lcg_step(s);
+          if ((s1 >> 47) == 0) break;  // light branch: a candidate
+          const uint64_t s3 = lcg_step(lcg_step(s1));
+          const float r2 = (float)((double)(uint32_t)(s3 >> 16) / 4294967296.0);
+          if (!(r2 <= 0.999f)) break;  // near-tangent BSDF sample: evaluate it
+          s = s3;
+          ++t;
+        }
+      }
+      Rng rr{s, 0};
+      Bsdf f = bsdf_of(me);
+      V3 nd;
+      const float pv = mixture_attempt(S, f, me.p, rr, nd);
+      lcg = rr.lcg;
+      tries = t + 1;
+      if (pv != 0 || tries >= kMixtureGuard) {
+        ndir = nd;
+        pdf = pv;
+        pend = false;
+      }
+    }
+    ++rounds;
+  }
+  return rounds;
+}
+
 // The camera ray of sample s_global of pixel `pix` with its per-path RNG streams
 // (SURVEY §8(d) seeding; Raytracing_n.cpp:827-836; camera::get_ray, camera.h:51-59).
 SRR_D void camera_ray(const SceneView& S, int pix, int s_global, double sx, double sy, int nx, int ny,
@@ -1931,6 +2035,7 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
     V3 d_atten = v3(0.f), d_n = v3(0.f), d_dir = v3(0.f);
     float d_pdf = 0;
     int d_tries = 0;
+    bool d_dead = false;
     if (g >= 0) {
       const WorldHit w = world_hit<MEDIA, TIMED ? (TR_BVH4_TIMED | (WL ? TR_WL : 0)) : TR>(S, r, rng, cx);
       if (TIMED) {
@@ -1964,6 +2069,7 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
           f.B = M.p[1];
           bsdf_prepare<false>(f, r.d);
           ds = diff_setup(f, h.p);
+          if (SRR_MIXTURE_SKIP) d_dead = bsdf_dead(S, f, h.p);
           (void)drand(rng);  // mixture_pdf ctor (pdf.h:175)
           d_n = h.n;
           diff = pend = true;
@@ -1987,7 +2093,15 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
     }
     if (__ballot(pend)) {
       const uint64_t tc = TIMED ? __builtin_amdgcn_s_memtime() : 0;
-      const int rounds = coop_mixture(S, ds, pend, d_tries, rng.lcg, d_dir, d_pdf);
+      // SRR_MIXTURE_SKIP 1: per-lane loops passing over dead draws; 2: one such
+      // round, then the wave-cooperative loop for what is left; 0: cooperative only
+      int rounds = 0;
+      if (SRR_MIXTURE_SKIP == 1) {
+        rounds = skip_mixture(S, ds, d_dead, pend, d_tries, rng.lcg, d_dir, d_pdf);
+      } else {
+        if (SRR_MIXTURE_SKIP == 2) rounds = skip_mixture(S, ds, d_dead, pend, d_tries, rng.lcg, d_dir, d_pdf, 1);
+        if (__ballot(pend)) rounds += coop_mixture(S, ds, pend, d_tries, rng.lcg, d_dir, d_pdf);
+      }
       if (TIMED) {
         tp[6] += __builtin_amdgcn_s_memtime() - tc;
         tp[7] += rounds;
