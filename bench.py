@@ -209,7 +209,7 @@ def main():
         kernel_name = ("k_trace (wavefront engine)" if wave else
                        "k_paths (path-resident persistent kernel: trace + shade)")
         traffic = None
-        pmc = os.path.join(ROOT, "profiles", f"pmc_{a.scene}.json")
+        pmc = os.path.join(ROOT, "profiles", f"pmc_{a.scene}{key[len(CONFIG_KEY[a.scene]):]}.json")
         if os.path.exists(pmc):
             pj = json.load(open(pmc))
             if pj.get("kernel", "") in kernel_name:
