@@ -33,6 +33,7 @@ struct SceneView {  // device pointers into the flattened tables (device_scene.h
   const int32_t* perlin_perm;
   const DLight* lights;
   int n_lights;
+  float light_weight;  // hitable_list::pdf_value's weight, (float)(1.0 / n_lights) (hitable_list.h:55)
   const DCamera* cam;
   // the world traversal's and shading's small tables packed in one blob (16-B
   // aligned pieces) that the kernels copy to LDS: byte offsets of objs, xforms,

@@ -1086,7 +1086,7 @@ __device__ __noinline__ float light_pdf_other(const SceneView& S, const DLight& 
 }
 
 SRR_D float lights_pdf(const SceneView& S, V3 o, V3 v) {
-  float weight = 1.0 / S.n_lights;
+  const float weight = S.light_weight;  // 1.0 / n (a double division), made once on the host
   float sum = 0;
   for (int k = 0; k < S.n_lights; ++k) sum += weight * light_pdf_one(S, S.lights[k], o, v);
   return sum;
@@ -2471,6 +2471,7 @@ __global__ void k_kat(int kind, int n, int w, float* rec, const float* aux, cons
       S.stris = kt.stris;
       S.lights = kt.lights;
       S.n_lights = kt.n_lights;
+      S.light_weight = kt.n_lights > 0 ? (float)(1.0 / kt.n_lights) : 0.f;
       Rng rng{kat_lcg(r + 3), 0};
       const V3 o = kat3(r);
       V3 d1, d2;

@@ -114,6 +114,7 @@ int renderer_create(const Scene& sc, int device, srr_renderer** out, std::string
   V.perlin_perm = pp;
   V.lights = li;
   V.n_lights = (int)F.lights.size();
+  V.light_weight = V.n_lights > 0 ? (float)(1.0 / V.n_lights) : 0.f;
   V.cam = cm;
   r->has_meshes = !F.meshes.empty() || !F.obvhs.empty();
   r->diffuse_only = true;
