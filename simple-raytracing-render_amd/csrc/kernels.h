@@ -21,6 +21,7 @@ struct SceneView {  // device pointers into the flattened tables (device_scene.h
   const float4* nodes;  // 2 float4 per BVH2 node: lo (min.xyz, skip), hi (max.xyz, leaf)
   const float4* node4;  // 8 float4 per 4-wide node (device_scene.h), breadth-first per mesh
   int node4_lds;        // leading nodes the path kernel keeps in LDS (<= kPathsLdsNodes)
+  int quad_trace;       // k_paths traces meshes quad-cooperatively (BVH4 larger than an XCD's L2)
   const float4* tri_pos;  // 4 float4 per triangle: p0, p1, p2, pad
   const TriShade* tri_shade;
   const DMedium* media;
@@ -104,7 +105,10 @@ struct PathWork {
 constexpr int kPathsGlobalStack = 56;  // global stack entries per lane beyond the LDS ones
 
 constexpr int kPathsWorldLdsBytes = 8192;  // == kernels.hip kWorldLdsBytes
-constexpr int kPathsLdsNodes = 96;         // BVH4 nodes cached in LDS by k_paths (12 KB)
+#ifndef SRR_LDS_NODES
+#define SRR_LDS_NODES 96
+#endif
+constexpr int kPathsLdsNodes = SRR_LDS_NODES;  // BVH4 nodes cached in LDS by k_paths (128 B each)
 void dump_trace_timing();
 int paths_lanes_per_device(const SceneView& S, int device);  // persistent grid capacity
 void launch_paths(const SceneView& S, const PathWork& W, int all_families, hipStream_t st);

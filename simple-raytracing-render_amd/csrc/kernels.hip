@@ -212,10 +212,18 @@ constexpr int kStack = 8;  // LDS stack entries per ray; deeper -> exact BVH2 re
 constexpr int kWorldLdsBytes = kPathsWorldLdsBytes;  // world tables staged in LDS up to this size
 constexpr unsigned long long kTimingCap = 1 << 16;  // SRR_TIMING wave records
 
+// LDS pointers in the LDS address space: generic pointers to the stacks let the
+// backend merge LDS and global-extension stack addresses into one flat pointer,
+// whose null check it can emit as an illegal compare on gfx950
+template <class T>
+using lds_ptr = __attribute__((address_space(3))) T*;
+template <class T>
+SRR_D lds_ptr<T> to_lds(T* p) { return (lds_ptr<T>)(uint32_t)(uintptr_t)p; }
+
 struct TraceCtx {
   unsigned long long* ctr;  // optional counters: boxes tested, triangle tests, stack overflows
-  int* st_node;    // this thread's LDS stack (stride kTraceBlock)
-  float* st_t;     // entry distance of each stacked node
+  lds_ptr<int> st_node;    // this thread's LDS stack (stride kTraceBlock)
+  lds_ptr<float> st_t;     // entry distance of each stacked node
   const __attribute__((address_space(3))) f32x4* lds_nodes = nullptr;  // LDS copy of node4[0, lds_count) (k_paths)
   int lds_count = 0;
   int st_cap = kStack;                   // stack entries used (<= kStack; SRR_STACK_CAP tests the re-walk)
@@ -411,6 +419,223 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
   return found;
 }
 
+// ------------------------------------------------ quad-cooperative traversal
+// In a path kernel wave most rays miss a mesh's root box (C2: 87 % of world rays
+// never enter the teapot's), and the few that enter hold the whole wave for their
+// 10-40 node steps.  mesh_hit4_quad gives each entering ray a hardware quad of
+// lanes (up to 16 rays per round): lane c of the quad tests child c of the node
+// (the reference's slab arithmetic; leaf children test their 1-2 triangles), the
+// quad reduces the hits with `wins` (a strict total order on (t, index), so any
+// reduction order gives the fold's winner) and orders its inner children nearest
+// first through DPP exchanges, and the quad's lane 0 lends its LDS stack (and
+// global extension).  Same visit rules, pruning and result as mesh_hit4; a quad
+// whose stack overflows leaves its ray to the exact BVH2 re-walk.
+constexpr int TR_QUAD = 32;
+
+template <int CTRL>
+SRR_D int quad_dpp(int x) { return __builtin_amdgcn_update_dpp(x, x, CTRL, 0xF, 0xF, false); }
+template <int CTRL>
+SRR_D float quad_dpp(float x) { return __int_as_float(quad_dpp<CTRL>(__float_as_int(x))); }
+constexpr int kQuadXor1 = 0xB1, kQuadXor2 = 0x4E;  // quad_perm [1,0,3,2], [2,3,0,1]
+template <int K>
+constexpr int kQuadBcast = K * 0x55;               // quad_perm [K,K,K,K]
+
+// the quad's winning candidate among its four lanes' (f, t, i)
+SRR_D void quad_best(bool& f, float& t, int& i) {
+#define SRR_QSTEP(CTRL)                                                      \
+  {                                                                          \
+    const bool of = quad_dpp<CTRL>((int)f) != 0;                             \
+    const float ot = quad_dpp<CTRL>(t);                                      \
+    const int oi = quad_dpp<CTRL>(i);                                        \
+    if (of && (!f || wins(ot, oi, t, i))) { f = true; t = ot; i = oi; }       \
+  }
+  SRR_QSTEP(kQuadXor1) SRR_QSTEP(kQuadXor2)
+#undef SRR_QSTEP
+}
+
+template <bool PRUNE>
+SRR_D bool mesh_hit4_quad(const SceneView& S, const DMesh& m, const Ray& r, float tmin, float tmax, bool is_medium,
+                          MeshHit& out, const TraceCtx& cx) {
+  const V3 inv = v3(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+  // every lane tests the mesh's root box -- the reference's bvh_node root, whose
+  // own box test comes first in bvh.h:64-66 -- itself
+  const bool want = slab(S.nodes[2 * m.node_off], S.nodes[2 * m.node_off + 1], r.o, inv, tmin, tmax);
+  if (__ballot(1) != ~0ull) {  // not a full wave (its last paths): per lane
+    if (!want) return false;
+    return mesh_hit4<PRUNE>(S, m, r, tmin, tmax, is_medium, out, cx);
+  }
+  const int lane = __lane_id(), q = lane >> 2, c = lane & 3;
+  const float len = length(r.d);
+  const V3 dir = r.d / len;
+  const float to_param = kPruneSlack / len;
+  // quad lane 0's stacks serve its quad (entry e of lane l - c is cx.st_*[e * kTraceBlock - c])
+  const int gslot = cx.slot - c;
+  bool found_me = false, redo_me = false;
+  float t_me = 0;
+  int i_me = -1;
+  uint64_t W = __ballot(want);
+  while (W) {
+    // this round: up to 16 wanting lanes, quad k serving the k-th
+    int owner = 0, nb = 0;
+    uint64_t Wr = 0;
+    for (; nb < 16 && W; ++nb) {  // wave-uniform: the round's lanes in order
+      const int l = __ffsll((unsigned long long)W) - 1;
+      W &= W - 1;
+      Wr |= 1ull << l;
+      if (q == nb) owner = l;
+    }
+    bool run = q < nb;
+    // the owner's ray
+    const V3 o = v3(__shfl(r.o.x, owner), __shfl(r.o.y, owner), __shfl(r.o.z, owner));
+    const V3 iv = v3(__shfl(inv.x, owner), __shfl(inv.y, owner), __shfl(inv.z, owner));
+    const V3 dr = v3(__shfl(dir.x, owner), __shfl(dir.y, owner), __shfl(dir.z, owner));
+    const float q_tmin = __shfl(tmin, owner), q_tmax = __shfl(tmax, owner), q_tp = __shfl(to_param, owner);
+    const bool q_med = __shfl((int)is_medium, owner) != 0;
+    int node = m.node4_off, sp = 0;
+    float bound = q_tmax, best_t = 0;
+    int best_i = -1;
+    bool found = false, overflow = false, deep = false;
+    while (__ballot(run)) {
+      if (run) {
+        // child c of the node
+        float lx, ly, lz, hx, hy, hz;
+        int ch;
+        if (node < cx.lds_count) {
+          const __attribute__((address_space(3))) float* N =
+              (const __attribute__((address_space(3))) float*)(cx.lds_nodes + 8 * node);
+          lx = N[c], ly = N[4 + c], lz = N[8 + c], hx = N[12 + c], hy = N[16 + c], hz = N[20 + c];
+          ch = __float_as_int(N[24 + c]);
+        } else {
+          const float* N = (const float*)(S.node4 + 8 * (size_t)node);
+          lx = N[c], ly = N[4 + c], lz = N[8 + c], hx = N[12 + c], hy = N[16 + c], hz = N[20 + c];
+          ch = __float_as_int(N[24 + c]);
+        }
+        float lo_ = -INFINITY, hi_ = INFINITY;
+#define SRR_QAX(L, H, O, I)                      \
+  {                                              \
+    float t0 = (L - O) * I, t1 = (H - O) * I;    \
+    bool sw = I < 0.0f;                          \
+    float n_ = sw ? t1 : t0, f_ = sw ? t0 : t1;  \
+    lo_ = n_ > lo_ ? n_ : lo_;                   \
+    hi_ = f_ < hi_ ? f_ : hi_;                   \
+  }
+        SRR_QAX(lx, hx, o.x, iv.x) SRR_QAX(ly, hy, o.y, iv.y) SRR_QAX(lz, hz, o.z, iv.z)
+#undef SRR_QAX
+        const float a_ = lo_ > q_tmin ? lo_ : q_tmin, b_ = hi_ < q_tmax ? hi_ : q_tmax;
+        const bool hit = !(b_ <= a_) && !(PRUNE && lo_ > bound);
+        // a leaf child: its triangles
+        bool cf = false;
+        float ct = 0;
+        int ci = -1;
+        if (hit && ch < 0 && ch != INT32_MIN) {
+          const int leaf = ~ch;
+          const int first = leaf >> 1, count = (leaf & 1) + 1;
+          for (int ti = first; ti < first + count; ++ti) {
+            const float4* tp = S.tri_pos + kTriStride * (size_t)ti;
+            const float4 a = tp[0], b = tp[1], cc = tp[2];
+            const V3 p0 = v3(a.x, a.y, a.z), p1 = v3(b.x, b.y, b.z), p2 = v3(cc.x, cc.y, cc.z);
+            float t, u, v;
+            bool h = tri_hit(p0, p1, p2, true, o, dr, t, u, v);
+            if (!h && q_med) h = tri_hit(p0, p1, p2, false, o, dr, t, u, v);
+            if (h && (!cf || wins(t, ti, ct, ci))) {
+              cf = true;
+              ct = t;
+              ci = ti;
+            }
+          }
+        }
+        quad_best(cf, ct, ci);
+        if (cf && (!found || wins(ct, ci, best_t, best_i))) {
+          found = true;
+          best_t = ct;
+          best_i = ci;
+        }
+        if (PRUNE && found && best_t * q_tp < bound) bound = best_t * q_tp;
+        // inner children that still overlap [tmin, bound], nearest first (ties: lower c)
+        const bool take = hit && ch >= 0 && !(PRUNE && lo_ > bound);
+        const float nk[4] = {quad_dpp<kQuadBcast<0>>(lo_), quad_dpp<kQuadBcast<1>>(lo_), quad_dpp<kQuadBcast<2>>(lo_),
+                             quad_dpp<kQuadBcast<3>>(lo_)};
+        const int tk = quad_dpp<kQuadBcast<0>>((int)take) | (quad_dpp<kQuadBcast<1>>((int)take) << 1) |
+                       (quad_dpp<kQuadBcast<2>>((int)take) << 2) | (quad_dpp<kQuadBcast<3>>((int)take) << 3);
+        const int ck[4] = {quad_dpp<kQuadBcast<0>>(ch), quad_dpp<kQuadBcast<1>>(ch), quad_dpp<kQuadBcast<2>>(ch),
+                           quad_dpp<kQuadBcast<3>>(ch)};
+        const int ntake = __popc(tk);
+        if (ntake > 0) {
+          int rank = 0, first_k = -1;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            if (!((tk >> k) & 1)) continue;
+            if (k != c && (nk[k] < lo_ || (nk[k] == lo_ && k < c))) ++rank;
+            if (first_k < 0) first_k = k;
+            else if (nk[k] < nk[first_k]) first_k = k;
+          }
+          if (take && rank > 0) {  // pushed farthest first: rank 1 ends on top
+            const int pos = sp + (ntake - 1 - rank);
+            if (pos < cx.st_cap) {
+              cx.st_node[pos * kTraceBlock - c] = ch;
+              cx.st_t[pos * kTraceBlock - c] = lo_;
+            } else if (pos < cx.st_cap + cx.gst_cap) {
+              cx.gst[(size_t)(pos - cx.st_cap) * cx.gst_stride + gslot] = make_int2(ch, __float_as_int(lo_));
+              deep = true;
+            } else {
+              overflow = true;
+            }
+          }
+          sp = min(sp + ntake - 1, cx.st_cap + cx.gst_cap);
+          node = ck[first_k];
+        } else {
+          int nx = -1;
+          while (sp > 0) {
+            --sp;
+            int cand;
+            float ctt;
+            if (sp < cx.st_cap) {
+              cand = cx.st_node[sp * kTraceBlock - c];
+              ctt = cx.st_t[sp * kTraceBlock - c];
+            } else {
+              const int2 e = cx.gst[(size_t)(sp - cx.st_cap) * cx.gst_stride + gslot];
+              cand = e.x;
+              ctt = __int_as_float(e.y);
+            }
+            if (!(PRUNE && ctt > bound)) {
+              nx = cand;
+              break;
+            }
+          }
+          if (nx < 0) run = false;
+          else node = nx;
+        }
+      }
+    }
+    // the quad's overflow / deep flags, then the result back to its owner
+    overflow = (quad_dpp<kQuadBcast<0>>((int)overflow) | quad_dpp<kQuadBcast<1>>((int)overflow) |
+                quad_dpp<kQuadBcast<2>>((int)overflow) | quad_dpp<kQuadBcast<3>>((int)overflow)) != 0;
+    deep = (quad_dpp<kQuadBcast<0>>((int)deep) | quad_dpp<kQuadBcast<1>>((int)deep) |
+            quad_dpp<kQuadBcast<2>>((int)deep) | quad_dpp<kQuadBcast<3>>((int)deep)) != 0;
+    const int my_q = __popcll(Wr & ((1ull << lane) - 1));  // owners: their quad
+    const int from = 4 * my_q;
+    const bool f_r = __shfl((int)found, from) != 0;
+    const float t_r = __shfl(best_t, from);
+    const int i_r = __shfl(best_i, from);
+    const bool o_r = __shfl((int)overflow, from) != 0;
+    const bool d_r = __shfl((int)deep, from) != 0;
+    if ((Wr >> lane) & 1) {
+      found_me = f_r;
+      t_me = t_r;
+      i_me = i_r;
+      redo_me = o_r;
+      if (cx.ovf && d_r) atomicAdd(cx.ovf + 1, 1ull);
+    }
+  }
+  if (redo_me) {  // rare: exact re-walk
+    if (cx.ovf) atomicAdd(cx.ovf, 1ull);
+    return mesh_hit<false>(S, m, r, tmin, tmax, is_medium, out, cx.ctr);
+  }
+  out.t = t_me;
+  out.tri = i_me;
+  return found_me;
+}
+
 // Instance chain (outermost first): the ray going in (hitable.h:44-52, 109-116,
 // 180-188; flip leaves the ray alone)
 template <int TR = 0>
@@ -541,6 +766,7 @@ SRR_D bool basic_hit(const SceneView& S, const DObj& ob, const Ray& lr, float tm
       const DMesh m = wload<TR>(S.meshes, ob.idx);
       bool hit;
       if (tr_mode(TR) == TR_BVH2) hit = mesh_hit<false>(S, m, lr, tmin, tmax, is_medium, mh, cx.ctr);
+      else if (TR & TR_QUAD) hit = mesh_hit4_quad<tr_mode(TR) != TR_BVH4>(S, m, lr, tmin, tmax, is_medium, mh, cx);
       else hit = mesh_hit4<tr_mode(TR) != TR_BVH4, tr_mode(TR) == TR_BVH4_TIMED>(S, m, lr, tmin, tmax, is_medium, mh, cx);
       if (!hit) return false;
       h.t = mh.t;
@@ -1622,8 +1848,8 @@ __global__ void __launch_bounds__(kTraceBlock) k_trace(SceneView S0, PathState P
   if constexpr (tr_mode(TR) != TR_BVH2) {
     __shared__ int s_node[kStack * kTraceBlock];
     __shared__ float s_t[kStack * kTraceBlock];
-    cx.st_node = s_node + threadIdx.x;
-    cx.st_t = s_t + threadIdx.x;
+    cx.st_node = to_lds(s_node + threadIdx.x);
+    cx.st_t = to_lds(s_t + threadIdx.x);
   }
   const uint64_t t_staged = tr_mode(TR) == TR_BVH4_TIMED ? __builtin_amdgcn_s_memtime() : 0;
   uint64_t t_ray = t_staged, t_hit = t_staged;
@@ -1688,8 +1914,8 @@ __global__ void __launch_bounds__(kTraceBlock) k_probe(SceneView S, PathState P,
   if constexpr (TR != TR_BVH2) {
     __shared__ int s_node[kStack * kTraceBlock];
     __shared__ float s_t[kStack * kTraceBlock];
-    cx.st_node = s_node + threadIdx.x;
-    cx.st_t = s_t + threadIdx.x;
+    cx.st_node = to_lds(s_node + threadIdx.x);
+    cx.st_t = to_lds(s_t + threadIdx.x);
   }
   int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= *count) return;
@@ -1920,7 +2146,7 @@ SRR_D float4 rec_load(const float4* p) { return SRR_REC_NT ? ntl(p) : *p; }
 constexpr int kPathsBlock = 256;
 constexpr unsigned long long kPoolChunk = 64;  // path indices a wave takes per cursor atomic
 
-template <bool MEDIA, bool ALLFAM, int MINB, bool TIMED = false, bool WL = true>
+template <bool MEDIA, bool ALLFAM, int MINB, bool TIMED = false, bool WL = true, bool QUAD = false>
 __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathWork W) {
   // TIMED (diagnostics): per-wave cycles in refill / world hit (mesh part) / record+scatter / fold
   uint64_t tp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1928,7 +2154,8 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
   SceneView S = S0;
   // WL: world tables staged in LDS (they fit in kWorldLdsBytes); otherwise read
   // from global memory (large object lists, e.g. random_scene's ~490 spheres)
-  constexpr int TR = TR_BVH4_PRUNE | (WL ? TR_WL : 0);
+  // QUAD: meshes traced by mesh_hit4_quad (large BVHs, SceneView::quad_trace)
+  constexpr int TR = TR_BVH4_PRUNE | (WL ? TR_WL : 0) | (QUAD ? TR_QUAD : 0);
   if constexpr (WL) {
     __shared__ uint4 s_world[kWorldLdsBytes / 16];
     for (int i = threadIdx.x; i < S0.world_words; i += blockDim.x) s_world[i] = S0.world_blob[i];
@@ -1950,8 +2177,8 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
   __shared__ float4 s_n4[kPathsLdsNodes * 8];
   for (int i = threadIdx.x; i < S0.node4_lds * 8; i += blockDim.x) s_n4[i] = S0.node4[i];
   __syncthreads();
-  TraceCtx cx{nullptr, s_node + threadIdx.x, s_t + threadIdx.x};
-  cx.lds_nodes = (const __attribute__((address_space(3))) f32x4*)s_n4;
+  TraceCtx cx{nullptr, to_lds(s_node + threadIdx.x), to_lds(s_t + threadIdx.x)};
+  cx.lds_nodes = (const __attribute__((address_space(3))) f32x4*)to_lds(s_n4);
   cx.lds_count = S0.node4_lds;
   cx.st_cap = W.stack_cap;
   cx.ovf = W.counters + 11;
@@ -2663,8 +2890,9 @@ void launch_paths(const SceneView& S, const PathWork& W, int all_families, hipSt
   static const bool timed = getenv("SRR_PATHS_TIMING") != nullptr;
   static const bool force_global = getenv("SRR_WORLD_GLOBAL") != nullptr;  // A/B diagnostics
   if (force_global || S.world_words * 16 > dev::kWorldLdsBytes) {  // world tables too large for LDS: global reads
-#define SRR_LAUNCH_PATHS_G(M, A) \
-  hipLaunchKernelGGL((dev::k_paths<M, A, 4, false, false>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W)
+#define SRR_LAUNCH_PATHS_G(M, A)                                                                                      \
+  if (S.quad_trace) hipLaunchKernelGGL((dev::k_paths<M, A, 4, false, false, true>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W); \
+  else hipLaunchKernelGGL((dev::k_paths<M, A, 4, false, false>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W)
     if (S.has_media) {
       if (all_families) SRR_LAUNCH_PATHS_G(true, true);
       else SRR_LAUNCH_PATHS_G(true, false);
@@ -2677,6 +2905,7 @@ void launch_paths(const SceneView& S, const PathWork& W, int all_families, hipSt
   }
 #define SRR_LAUNCH_PATHS(M, A, B)                                                                      \
   if (timed) hipLaunchKernelGGL((dev::k_paths<M, A, 4, true>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W); \
+  else if (S.quad_trace && B == 4) hipLaunchKernelGGL((dev::k_paths<M, A, 4, false, true, true>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W); \
   else hipLaunchKernelGGL((dev::k_paths<M, A, B>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W)
 #define SRR_LAUNCH_PATHS_B(M, A)                          \
   switch (paths_min_blocks()) {                           \

@@ -28,8 +28,11 @@ def _save_diag(name, bad, out):
                         rays=out["rays"][bad], mean=out["mean"][bad])
 
 
-@pytest.mark.parametrize("engine", ["paths"])
-def test_c2_full_frame_is_the_reference_frame(engine):
+@pytest.mark.parametrize("quad", ["0", "1"])
+def test_c2_full_frame_is_the_reference_frame(quad, monkeypatch):
+    """quad=1 forces the quad-cooperative mesh traversal (kernels.hip
+    mesh_hit4_quad) onto the L2-resident teapot, which by default runs per lane."""
+    monkeypatch.setenv("SRR_QUAD", quad)
     name = "c2_full"
     m = fullframe.meta(name)
     want = fullframe.load(name)

@@ -50,6 +50,20 @@ def test_paths_match_reference(name, engine):
     assert ic["mean_rel"] <= 0.005, ic
 
 
+@pytest.mark.parametrize("name", sorted(META))
+def test_quad_traversal_matches_reference(name, monkeypatch):
+    """The quad-cooperative mesh traversal (kernels.hip mesh_hit4_quad; the
+    default only for BVHs larger than an XCD's L2) forced on every golden scene:
+    the same paths, bit for bit, and the same world rays as the reference."""
+    monkeypatch.setenv("SRR_QUAD", "1")
+    m, text, gp, gr, gi = golden(name)
+    out = capi.Renderer(text).render(m["nx"], m["ny"], m["spp"], m["max_depth"], keep_paths=True)
+    pc = parity.compare_paths(out["paths"], gp)
+    assert pc["bitexact"] >= parity.MIN_BITEXACT, pc
+    assert (out["rays"] == gr).all()
+    assert out["stats"]["world_rays"] == m["world_rays"]
+
+
 @pytest.mark.parametrize("factory", [scenes.s2_cornell_teapot, lambda: scenes.s3_cornell_teapot_microfacet("metal")])
 def test_engines_render_identical_images(factory):
     """The path-resident and wavefront engines run the same per-path arithmetic
@@ -216,17 +230,20 @@ def test_model_file_scene_matches_oracle(tmp_path):
     assert pc["bitexact"] >= parity.MIN_BITEXACT, pc
 
 
+@pytest.mark.parametrize("quad", ["0", "1"])
 @pytest.mark.parametrize("gstack", ["0", "1"])
 @pytest.mark.parametrize("name", ["s4_d40", "s5_d40", "s2_d100"])
-def test_stack_overflow_rewalk_matches_reference(name, gstack, monkeypatch):
+def test_stack_overflow_rewalk_matches_reference(name, gstack, quad, monkeypatch):
     """The BVH4 traversal's LDS stack holds kStack = 8 entries, extended in global
     memory by kPathsGlobalStack more; a ray that needs more re-walks the mesh with
     the exact stackless BVH2 (kernels.hip mesh_hit4).  SRR_STACK_CAP=1 (read per
     render call) sends most mesh rays of the 102,400- and 640,000-triangle goldens
     through the global extension (SRR_GSTACK=1) or, without it (SRR_GSTACK=0),
     through the re-walk: every path still bit-identical to the reference, and the
-    counters show that path really ran."""
+    counters show that path really ran.  SRR_QUAD (read when the scene is
+    uploaded) runs both the per-lane and the quad-cooperative traversal."""
     m, text, gp, gr, gi = golden(name)
+    monkeypatch.setenv("SRR_QUAD", quad)
     monkeypatch.setenv("SRR_STACK_CAP", "1")
     monkeypatch.setenv("SRR_GSTACK", gstack)
     out = capi.Renderer(text).render(m["nx"], m["ny"], m["spp"], m["max_depth"], keep_paths=True)
