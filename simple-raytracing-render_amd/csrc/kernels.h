@@ -102,6 +102,10 @@ struct PathWork {
   int2* gstack;           // the stack's global extension [gstack_cap][lanes] (deep meshes), or nullptr
   int gstack_cap;
 };
+#ifndef SRR_KSTACK
+#define SRR_KSTACK 8
+#endif
+constexpr int kPathsLdsStack = SRR_KSTACK;  // LDS traversal stack entries per lane (kernels.hip kStack)
 constexpr int kPathsGlobalStack = 56;  // global stack entries per lane beyond the LDS ones
 
 constexpr int kPathsWorldLdsBytes = 8192;  // == kernels.hip kWorldLdsBytes

@@ -208,7 +208,7 @@ SRR_D T wload(const T* p, int i) {
   else return cload(p, i);
 }
 constexpr int kTraceBlock = 256;
-constexpr int kStack = 8;  // LDS stack entries per ray; deeper -> exact BVH2 re-walk
+constexpr int kStack = kPathsLdsStack;  // LDS stack entries per ray; deeper -> global extension, then the exact BVH2 re-walk
 constexpr int kWorldLdsBytes = kPathsWorldLdsBytes;  // world tables staged in LDS up to this size
 constexpr unsigned long long kTimingCap = 1 << 16;  // SRR_TIMING wave records
 

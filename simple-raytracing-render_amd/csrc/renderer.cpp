@@ -355,8 +355,8 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
     w.rec = r->pw_rec;
     w.err = (int*)(r->pw_ctr + 2);
     w.lanes = (int)std::min<int64_t>(r->pw_lanes, ((w.n_paths + 255) / 256) * 256);
-    w.stack_cap = 8;  // kernels.hip kStack
-    if (const char* e = getenv("SRR_STACK_CAP")) w.stack_cap = std::max(1, std::min(8, atoi(e)));
+    w.stack_cap = kPathsLdsStack;  // kernels.hip kStack
+    if (const char* e = getenv("SRR_STACK_CAP")) w.stack_cap = std::max(1, std::min(kPathsLdsStack, atoi(e)));
     w.gstack = gst_cap ? r->pw_gstack : nullptr;
     w.gstack_cap = gst_cap;
     RCHK(hipMemsetAsync(w.cursor, 0, sizeof(unsigned long long), st));
