@@ -22,6 +22,7 @@ struct SceneView {  // device pointers into the flattened tables (device_scene.h
   const float4* node4;  // 8 float4 per 4-wide node (device_scene.h), breadth-first per mesh
   int node4_lds;        // leading nodes the path kernel keeps in LDS (<= kPathsLdsNodes)
   int quad_trace;       // k_paths traces meshes quad-cooperatively (BVH4 larger than an XCD's L2)
+  int quad_max;         // ...when at most this many lanes of the wave enter the mesh (else per lane)
   const float4* tri_pos;  // 4 float4 per triangle: p0, p1, p2, pad
   const TriShade* tri_shade;
   const DMedium* media;

@@ -474,6 +474,10 @@ SRR_D bool mesh_hit4_quad(const SceneView& S, const DMesh& m, const Ray& r, floa
   float t_me = 0;
   int i_me = -1;
   uint64_t W = __ballot(want);
+  if (__popcll(W) > S.quad_max) {  // many rays enter: one per lane
+    if (!want) return false;
+    return mesh_hit4<PRUNE>(S, m, r, tmin, tmax, is_medium, out, cx);
+  }
   while (W) {
     // this round: up to 16 wanting lanes, quad k serving the k-th
     int owner = 0, nb = 0;
