@@ -345,25 +345,27 @@ int srr_renderer_create(const srr_scene* sc, int device, srr_renderer** out) {
 
 void srr_renderer_destroy(srr_renderer* r) { delete r; }
 
-static bool tile_of(const srr_params* p, int pix) {
-  int tile = p->tile > 0 ? p->tile : 32;
-  int row = pix / p->nx, col = pix % p->nx;
-  int tiles_x = (p->nx + tile - 1) / tile;
-  int t = (row / tile) * tiles_x + col / tile;
-  return (t % p->shard_count) == p->shard_index;
-}
-
 int64_t srr_shard_pixels(const srr_params* p, int32_t* out) {
   if (!p || p->nx <= 0 || p->ny <= 0 || p->shard_count < 1 || p->shard_index < 0 ||
       p->shard_index >= p->shard_count)
     return fail(SRR_EINVAL, "bad params");
-  // shard tiles round-robin; pixels in PPM order within the shard
+  // shard tiles round-robin: tile t = (row / tile) * tiles_x +
+  // col / tile belongs to shard t % shard_count; pixels in PPM order within the
+  // shard, emitted row by row as runs of a tile's columns
+  const int tile = p->shard_count == 1 ? p->nx : (p->tile > 0 ? p->tile : 32);
+  const int tiles_x = (p->nx + tile - 1) / tile;
   int64_t n = 0;
-  for (int pix = 0; pix < p->nx * p->ny; ++pix)
-    if (p->shard_count == 1 || tile_of(p, pix)) {
-      if (out) out[n] = pix;
-      ++n;
+  for (int row = 0; row < p->ny; ++row) {
+    const int t0 = (row / tile) * tiles_x;
+    for (int tc = 0; tc < tiles_x; ++tc) {
+      if ((t0 + tc) % p->shard_count != p->shard_index) continue;
+      const int c1 = std::min(p->nx, (tc + 1) * tile);
+      for (int col = tc * tile; col < c1; ++col) {
+        if (out) out[n] = row * p->nx + col;
+        ++n;
+      }
     }
+  }
   return n;
 }
 
@@ -372,13 +374,23 @@ int srr_render_device(srr_renderer* r, const srr_params* p, float* d_mean, srr_s
   if (p->spp < 1 || p->max_depth < 0 || p->max_depth > 64) return fail(SRR_EINVAL, "spp >= 1, 0 <= max_depth <= 64");
   if (p->sample_begin < 0 || p->sample_begin > INT32_MAX - p->spp)
     return fail(SRR_EINVAL, "sample_begin must be >= 0 and sample_begin + spp must fit in int32");
-  int64_t npix = srr_shard_pixels(p, nullptr);
+  // the shard's pixel list is built and uploaded once per shard (srr_renderer::pix_key)
+  const int key[5] = {p->nx, p->ny, p->shard_index, p->shard_count, p->tile};
+  const bool held = std::equal(key, key + 5, r->pix_key);
+  int64_t npix = held ? r->pix_n : srr_shard_pixels(p, nullptr);
   if (npix < 0) return (int)npix;
-  std::vector<int32_t> pix(npix);
-  srr_shard_pixels(p, pix.data());
+  std::vector<int32_t> pix;
+  if (!held) {
+    pix.resize(npix);
+    srr_shard_pixels(p, pix.data());
+  }
   std::string err;
-  int rc = render_device(r, p, pix.data(), npix, d_mean, stats, err);
+  int rc = render_device(r, p, held ? nullptr : pix.data(), npix, d_mean, stats, err);
   if (rc < 0) return fail(rc, err);
+  if (!held) {
+    std::copy(key, key + 5, r->pix_key);
+    r->pix_n = npix;
+  }
   return 0;
 }
 
@@ -417,6 +429,7 @@ int srr_accum_set(srr_renderer* r, const float* sums, int64_t npix, int64_t samp
   if (!r || !sums || npix <= 0 || samples < 0) return fail(SRR_EINVAL, "bad accumulator state");
   HIPCHK(hipSetDevice(r->device));
   if ((size_t)npix > r->pix_cap) {
+    r->pix_key[0] = -1;  // the held pixel list goes with the buffer
     (void)hipFree(r->pixels);
     (void)hipFree(r->acc);
     r->pixels = nullptr;

@@ -236,6 +236,42 @@ static int begin_accum(srr_renderer* r, const srr_params* p, int64_t npix, hipSt
   return 0;
 }
 
+// Stages a shard's pixel list on the device (with the frame accumulator sized
+// to it); an identity list is not uploaded (the path engine does not read it).
+static hipError_t stage_pixels(srr_renderer* r, const int32_t* pix, int64_t npix, bool identity) {
+  r->pix_key[0] = -1;  // srr_render_device sets the key once the render succeeds
+  if ((size_t)npix > r->pix_cap) {
+    (void)hipFree(r->pixels);
+    (void)hipFree(r->acc);
+    r->pixels = nullptr;
+    r->acc = nullptr;
+    r->pix_cap = 0;
+    hipError_t e = hipMalloc((void**)&r->pixels, npix * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMalloc((void**)&r->acc, 3 * npix * sizeof(float));
+    if (e != hipSuccess) return e;
+    r->pix_cap = npix;
+  }
+  r->pix_identity = identity;
+  return identity ? hipSuccess : hipMemcpy(r->pixels, pix, npix * sizeof(int32_t), hipMemcpyHostToDevice);
+}
+
+// The device Sobol set holds the first sobol_n points; the set is a
+// prefix-stable sequence (tests/test_dist_gloo.py), so it is generated and
+// uploaded only when a render needs more points than it holds.
+static hipError_t ensure_sobol(srr_renderer* r, int n_sobol) {
+  if (n_sobol <= r->sobol_n) return hipSuccess;
+  (void)hipFree(r->sobol);
+  r->sobol = nullptr;
+  r->sobol_n = 0;
+  hipError_t e = hipMalloc((void**)&r->sobol, 2 * (size_t)n_sobol * sizeof(double));
+  if (e != hipSuccess) return e;
+  std::vector<double> sp(2 * (size_t)n_sobol);
+  sobol2((unsigned)n_sobol, sp.data());
+  e = hipMemcpy(r->sobol, sp.data(), sp.size() * sizeof(double), hipMemcpyHostToDevice);
+  if (e == hipSuccess) r->sobol_n = n_sobol;
+  return e;
+}
+
 // Invalidates the running sums unless the render that began them committed:
 // a failed render leaves partial sums that no SRR_FLAG_CONTINUE may build on.
 struct AccCommit {
@@ -256,28 +292,13 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
   const auto t_host0 = std::chrono::steady_clock::now();
   srr_stats s{};
   // pixels: identity for a whole frame, else the shard list
-  bool identity = p->shard_count <= 1;
-  for (int64_t i = 0; identity && i < npix; i += std::max<int64_t>(1, npix / 64)) identity = pix[i] == i;
-  if ((size_t)npix > r->pix_cap) {
-    (void)hipFree(r->pixels);
-    (void)hipFree(r->acc);
-    r->pixels = nullptr;
-    r->acc = nullptr;
-    RCHK(hipMalloc((void**)&r->pixels, npix * sizeof(int32_t)));
-    RCHK(hipMalloc((void**)&r->acc, 3 * npix * sizeof(float)));
-    r->pix_cap = npix;
+  bool identity = r->pix_identity;
+  if (pix) {  // a new pixel list (else the renderer holds this shard's already)
+    identity = p->shard_count <= 1;
+    for (int64_t i = 0; identity && i < npix; i += std::max<int64_t>(1, npix / 64)) identity = pix[i] == i;
+    RCHK(stage_pixels(r, pix, npix, identity));
   }
-  if (!identity) RCHK(hipMemcpy(r->pixels, pix, npix * sizeof(int32_t), hipMemcpyHostToDevice));
-  const int n_sobol = p->sample_begin + p->spp;
-  if (n_sobol > r->sobol_n) {
-    (void)hipFree(r->sobol);
-    r->sobol = nullptr;
-    RCHK(hipMalloc((void**)&r->sobol, 2 * (size_t)n_sobol * sizeof(double)));
-    r->sobol_n = n_sobol;
-  }
-  std::vector<double> sp(2 * (size_t)n_sobol);
-  sobol2((unsigned)n_sobol, sp.data());
-  RCHK(hipMemcpy(r->sobol, sp.data(), sp.size() * sizeof(double), hipMemcpyHostToDevice));
+  RCHK(ensure_sobol(r, p->sample_begin + p->spp));
   if (keep) {
     size_t need = (size_t)npix * p->spp;
     if (need > r->keep_cap) {
@@ -432,28 +453,15 @@ int render_device(srr_renderer* r, const srr_params* p, const int32_t* pix, int6
     visits = r->visits;
   }
   // frame buffers
-  if ((size_t)npix > r->pix_cap) {
-    (void)hipFree(r->pixels);
-    (void)hipFree(r->acc);
-    r->pixels = nullptr;
-    r->acc = nullptr;
-    RCHK(hipMalloc((void**)&r->pixels, npix * sizeof(int32_t)));
-    RCHK(hipMalloc((void**)&r->acc, 3 * npix * sizeof(float)));
-    r->pix_cap = npix;
+  if (pix) RCHK(stage_pixels(r, pix, npix, false));
+  else if (r->pix_identity) {  // the path engine skipped the upload of an identity list
+    std::vector<int32_t> id((size_t)npix);
+    for (int64_t i = 0; i < npix; ++i) id[i] = (int32_t)i;
+    RCHK(stage_pixels(r, id.data(), npix, false));
   }
-  RCHK(hipMemcpy(r->pixels, pix, npix * sizeof(int32_t), hipMemcpyHostToDevice));
   // Sobol points of the global sample range [sample_begin, sample_begin + spp):
   // the set is a prefix-stable sequence, so a sample shard reads its own slice.
-  const int n_sobol = p->sample_begin + p->spp;
-  if (n_sobol > r->sobol_n) {
-    (void)hipFree(r->sobol);
-    r->sobol = nullptr;
-    RCHK(hipMalloc((void**)&r->sobol, 2 * (size_t)n_sobol * sizeof(double)));
-    r->sobol_n = n_sobol;
-  }
-  std::vector<double> sp(2 * (size_t)n_sobol);
-  sobol2((unsigned)n_sobol, sp.data());
-  RCHK(hipMemcpy(r->sobol, sp.data(), sp.size() * sizeof(double), hipMemcpyHostToDevice));
+  RCHK(ensure_sobol(r, p->sample_begin + p->spp));
   if (keep) {
     size_t need = (size_t)npix * p->spp;
     if (need > r->keep_cap) {

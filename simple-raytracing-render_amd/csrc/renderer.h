@@ -78,6 +78,13 @@ struct srr_renderer {
   unsigned long long* pw_ctr = nullptr;  // [0] world rays, [1] path cursor
   int32_t* pixels = nullptr;
   size_t pix_cap = 0;
+  // the shard whose pixel list (srr_shard_pixels) the renderer holds: {nx, ny,
+  // shard_index, shard_count, tile}, its pixel count, and whether it is the
+  // identity (then `pixels` is not read); key[0] = -1: none.  srr_render_device
+  // passes pix = nullptr to render_device when the shard is this one.
+  int pix_key[5] = {-1, -1, -1, -1, -1};
+  int64_t pix_n = 0;
+  bool pix_identity = false;
   double* sobol = nullptr;
   int sobol_n = 0;
   float* raw_all = nullptr;
@@ -89,6 +96,8 @@ struct srr_renderer {
 
 namespace srr {
 int renderer_create(const Scene& s, int device, srr_renderer** out, std::string& err);
+// pix: the shard's npix pixel indices, or nullptr when the renderer already holds
+// them (srr_renderer::pix_key)
 int render_device(srr_renderer* r, const srr_params* p, const int32_t* pix, int64_t npix, float* d_mean,
                   srr_stats* stats, std::string& err);
 }  // namespace srr
