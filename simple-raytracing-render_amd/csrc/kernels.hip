@@ -2452,6 +2452,46 @@ __global__ void __launch_bounds__(256) k_accumulate_window16(const float4* sampl
     cy = acc[3 * (size_t)lp + 1];
     cz = acc[3 * (size_t)lp + 2];
   }
+  if (np == 256) {
+    // full block: the 12 loads of chunk s0 + 16 are in flight while the block
+    // sums chunk s0 out of LDS (same per-pixel order of additions)
+    float4 v[kQ];
+    const float4* base = sample4 + (size_t)p0 * spp_w * 3 / 4;
+    auto fetch = [&](int s0) {
+#pragma unroll
+      for (int j = 0; j < kQ; ++j) {
+        const int i = threadIdx.x + 256 * j, px = i / kQ, f4 = i - px * kQ;
+        v[j] = ntl(&base[((size_t)px * spp_w + s0) * 3 / 4 + f4]);
+      }
+    };
+    fetch(0);
+    for (int s0 = 0; s0 < spp_w; s0 += kAccChunk) {
+#pragma unroll
+      for (int j = 0; j < kQ; ++j) {
+        const int i = threadIdx.x + 256 * j, px = i / kQ, f4 = i - px * kQ;
+        float* d = &tile[px * (3 * kAccChunk + 1) + 4 * f4];
+        d[0] = v[j].x;
+        d[1] = v[j].y;
+        d[2] = v[j].z;
+        d[3] = v[j].w;
+      }
+      __syncthreads();
+      if (s0 + kAccChunk < spp_w) fetch(s0 + kAccChunk);
+      const float* t = &tile[threadIdx.x * (3 * kAccChunk + 1)];
+#pragma unroll
+      for (int k = 0; k < kAccChunk; ++k) {
+        cx += t[3 * k];
+        cy += t[3 * k + 1];
+        cz += t[3 * k + 2];
+      }
+      __syncthreads();
+    }
+    const size_t a = 3 * (size_t)lp;
+    acc[a] = cx;
+    acc[a + 1] = cy;
+    acc[a + 2] = cz;
+    return;
+  }
   for (int s0 = 0; s0 < spp_w; s0 += kAccChunk) {
     for (int i = threadIdx.x; i < np * kQ; i += 256) {
       const int px = i / kQ, f4 = i - px * kQ;
