@@ -146,8 +146,8 @@ typedef struct srr_params {
   int spp;             /* samples per pixel, ns (:41)                          */
   int max_depth;       /* maxDepth (:42)                                       */
   int tile;            /* tile edge for sharding, e.g. 32                      */
-  int shard_index;     /* this renderer renders tiles t with t % shard_count   */
-  int shard_count;     /*   == shard_index                       */
+  int shard_index;     /* this renderer renders tiles t (in tile row tr) with  */
+  int shard_count;     /*   (t + tr) % shard_count == shard_index */
   int batch_paths;     /* paths in flight per wavefront batch (0 = auto)       */
   uint64_t base_seed;  /* per-path seed salt; 0 = SURVEY §8(d) definition      */
   int flags;           /* SRR_FLAG_*                                           */

@@ -5,7 +5,9 @@ Every (pixel, sample) path is independent and the scene is read-only, so a
 frame shards with no exchange until the end.  Two plans:
 
 * ``tiles``   (strong scaling, a fixed frame; the default): rank k renders the
-  32x32 tiles t with t % world == k, all samples.  Frame end: one gather of
+  32x32 tiles t (in tile row tr) with (t + tr) % world == k, all samples: round
+  robin with each tile row rotated by one, so no rank gets whole tile columns
+  (srr_shard_pixels).  Frame end: one gather of
   the packed per-pixel means to rank 0, which scatters them into the image.
   Bitwise equal to the one-GPU image (each pixel's samples are summed on one
   GPU in sample order).
