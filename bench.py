@@ -8,8 +8,8 @@
 One step = one whole frame through the C-ABI (srr_render_device, inputs
 resident in HBM) on every rank, then the frame-end exchange over RCCL
 (srr/dist.py).  Default plan "tiles" (strong scaling, the
-north_star split): the BASELINE config's one 512x512x1024 frame, 32x32 tiles
-round-robin over the N GPUs, one gather of the tiles' means to rank 0 (the
+north_star split): the BASELINE config's one 512x512x1024 frame, 16x16 tiles
+(--tile) round-robin over the N GPUs (each tile row rotated by one), one gather of the tiles' means to rank 0 (the
 image is bitwise the 1-GPU image).  Plan "samples" (weak scaling): each GPU
 renders 512x512x1024 paths as its sample range of one N*1024-spp frame; one
 reduce of raw per-pixel sums.  A "sample" is one world ray segment (one
@@ -43,8 +43,11 @@ def parse():
     ap.add_argument("--ny", type=int, default=0)
     ap.add_argument("--spp", type=int, default=0)
     ap.add_argument("--batch-paths", type=int, default=0)
+    ap.add_argument("--tile", type=int, default=16,
+                    help="tile edge of the tiles plan: 16 measured better balanced than 32 at 4 and 8 GPUs "
+                         "(tools/shard_balance.py, profiles/r02/shard_balance_*.json)")
     ap.add_argument("--plan", default="tiles", choices=["tiles", "samples"],
-                    help="multi-GPU split: tiles = strong scaling, the north_star split (one frame, 32x32 tiles "
+                    help="multi-GPU split: tiles = strong scaling, the north_star split (one frame, --tile tiles "
                          "round-robin, one gather to rank 0; bitwise the 1-GPU image), samples = weak scaling "
                          "(each GPU renders spp samples of every pixel, one reduce of raw sums)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -152,7 +155,7 @@ def main():
     nx, ny, spp = a.nx or cfg["nx"], a.ny or cfg["ny"], a.spp or cfg["spp"]
     text = sc.text()
     rend = capi.Renderer(text, device=local)
-    sh = dist_frame.plan_shard(nx, ny, spp, cfg["max_depth"], rank, world, plan=a.plan, tile=32,
+    sh = dist_frame.plan_shard(nx, ny, spp, cfg["max_depth"], rank, world, plan=a.plan, tile=a.tile,
                                batch_paths=a.batch_paths, flags=capi.FLAG_COUNT_VISITS if a.count_visits else 0)
     ex = dist_frame.FrameExchange(sh, dev, dist if world > 1 else None)
 
@@ -229,7 +232,7 @@ def main():
             "data": "synthetic (scene built in code: Cornell box + tessellated Utah teapot)",
             "config": {"workload": f"{key}: {a.scene}{f' divs {a.divs}' if a.divs else ''} {nx}x{ny} {spp}spp "
                                    f"maxDepth {cfg['max_depth']}" + (
-                                   f", 32x32 tiles round-robin over {world} GPU(s), RCCL gather to rank 0 at frame end"
+                                   f", {a.tile}x{a.tile} tiles round-robin over {world} GPU(s), RCCL gather to rank 0 at frame end"
                                    if a.plan == "tiles" else
                                    f" per GPU; {world} GPU(s) render sample ranges of one {spp * world}spp frame, "
                                    f"RCCL reduce at frame end"),
