@@ -102,6 +102,7 @@ struct PathWork {
   int stack_cap;          // BVH4 traversal stack entries (kStack = 8; fewer forces the exact re-walk)
   int2* gstack;           // the stack's global extension [gstack_cap][lanes] (deep meshes), or nullptr
   int gstack_cap;
+  unsigned long long* wave_times;  // diagnostics (SRR_WAVE_TIMES): per wave [start, exit] s_memrealtime, or nullptr
 };
 #ifndef SRR_KSTACK
 #define SRR_KSTACK 8

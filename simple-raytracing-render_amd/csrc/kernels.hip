@@ -2155,6 +2155,7 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
   // TIMED (diagnostics): per-wave cycles in refill / world hit (mesh part) / record+scatter / fold
   uint64_t tp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t it = 0;
+  const uint64_t t_start = W.wave_times ? __builtin_amdgcn_s_memrealtime() : 0;
   SceneView S = S0;
   // WL: world tables staged in LDS (they fit in kWorldLdsBytes); otherwise read
   // from global memory (large object lists, e.g. random_scene's ~490 spheres)
@@ -2395,6 +2396,11 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
   unsigned long long tot = nrays;
   for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
   if (lane_id() == 0 && tot) atomicAdd(W.counters, tot);
+  if (W.wave_times && lane_id() == 0) {  // diagnostics: when this wave started and ran out of paths
+    const size_t wv = (size_t)(blockIdx.x * blockDim.x + threadIdx.x) / 64;
+    W.wave_times[2 * wv] = t_start;
+    W.wave_times[2 * wv + 1] = __builtin_amdgcn_s_memrealtime();
+  }
 }
 
 // acc[pixel] += the window's samples in sample order (the sum order of

@@ -353,6 +353,14 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
   }
   AccCommit commit{r};
   const bool all_fam = !r->diffuse_only;
+  // diagnostics (SRR_WAVE_TIMES=1): per-wave start / exit times of each k_paths launch
+  static const bool want_wave_times = getenv("SRR_WAVE_TIMES") != nullptr;
+  unsigned long long* wave_times = nullptr;
+  const int n_waves = (r->pw_lanes + 63) / 64;
+  if (want_wave_times) {
+    RCHK(hipMalloc((void**)&wave_times, 2 * (size_t)n_waves * sizeof(unsigned long long)));
+    RCHK(hipMemsetAsync(wave_times, 0, 2 * (size_t)n_waves * sizeof(unsigned long long), st));
+  }
   RCHK(hipEventRecord(r->ev_beg, st));
   double kernel_ms = 0;
   for (int s0 = 0; s0 < p->spp; s0 += W) {
@@ -382,6 +390,7 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
     if (const char* e = getenv("SRR_STACK_CAP")) w.stack_cap = std::max(1, std::min(kPathsLdsStack, atoi(e)));
     w.gstack = gst_cap ? r->pw_gstack : nullptr;
     w.gstack_cap = gst_cap;
+    w.wave_times = wave_times;
     RCHK(hipMemsetAsync(w.cursor, 0, sizeof(unsigned long long), st));
     RCHK(hipEventRecord(r->lanes[0].ev_t0, st));
     launch_paths(r->view, w, all_fam ? 1 : 0, st);
@@ -391,6 +400,24 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
     float ms = 0;
     RCHK(hipEventElapsedTime(&ms, r->lanes[0].ev_t0, r->lanes[0].ev_t1));
     kernel_ms += ms;
+    if (wave_times) {  // realtime clock: 100 MHz (10 ns ticks)
+      std::vector<unsigned long long> wt(2 * (size_t)n_waves);
+      RCHK(hipMemcpy(wt.data(), wave_times, wt.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+      std::vector<double> ex;
+      unsigned long long t0 = ~0ull;
+      for (int i = 0; i < n_waves; ++i)
+        if (wt[2 * i + 1]) t0 = std::min(t0, wt[2 * i]);
+      for (int i = 0; i < n_waves; ++i)
+        if (wt[2 * i + 1]) ex.push_back((wt[2 * i + 1] - t0) * 1e-5);  // ms
+      std::sort(ex.begin(), ex.end());
+      if (!ex.empty()) {
+        auto q = [&](double f) { return ex[std::min(ex.size() - 1, (size_t)(f * ex.size()))]; };
+        fprintf(stderr, "k_paths wave exits (ms after the first wave start, %zu waves, kernel %.3f ms): "
+                "min %.3f p10 %.3f p50 %.3f p90 %.3f p99 %.3f max %.3f\n", ex.size(), ms, ex.front(), q(0.1), q(0.5),
+                q(0.9), q(0.99), ex.back());
+      }
+      RCHK(hipMemsetAsync(wave_times, 0, wt.size() * sizeof(unsigned long long), st));
+    }
     s.trace_launches += 1;
   }
   const int64_t acc_total = r->acc_samples + p->spp;
@@ -401,6 +428,7 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
   RCHK(hipEventRecord(r->ev_end, st));
   RCHK(hipStreamSynchronize(st));
   RCHK(hipGetLastError());
+  if (wave_times) (void)hipFree(wave_times);
   unsigned long long ctr[16] = {0};
   RCHK(hipMemcpy(ctr, r->pw_ctr, sizeof(ctr), hipMemcpyDeviceToHost));
   if (getenv("SRR_PATHS_TIMING") && ctr[9]) {
