@@ -1567,6 +1567,10 @@ constexpr int kMixtureGuard = 100000;  // the sequential loop's attempt cap (sca
 #define SRR_COOP_ID0 0
 #endif
 constexpr int kMaxHelpers = SRR_COOP_HELPERS;  // attempts of one path per round
+#ifndef SRR_DEEP_TRIES
+#define SRR_DEEP_TRIES 32
+#endif
+constexpr int kDeepTries = SRR_DEEP_TRIES;  // past this many failed attempts a path takes every free lane
 
 // Runs to completion the loops of every lane with `pend` (converged wave, all 64
 // lanes active).  In: the lane's setup, its LCG state before attempt `tries`.
@@ -1582,6 +1586,10 @@ SRR_D int coop_mixture(const SceneView& S, const DiffSetup& me, bool& pend, int&
   bool first = SRR_COOP_ID0 != 0;
   while (F) {
     const int nF = __popcll(F);
+    // paths whose loop has failed kDeepTries times (e.g. a hit point in the light's
+    // own plane: every light sample runs parallel to it) may need up to the guard's
+    // 100,000 attempts; once every pending path is that deep, all 64 lanes help
+    const int cap = __ballot(pend && tries < kDeepTries) == 0 ? 64 : kMaxHelpers;
     const int rank = pend ? __popcll(F & lt) : nF + __popcll(~F & lt);
     DiffSetup d;
     int t0, k;
@@ -1590,7 +1598,7 @@ SRR_D int coop_mixture(const SceneView& S, const DiffSetup& me, bool& pend, int&
       d = me;
       t0 = tries;
       s = lcg;
-      k = pend ? 0 : kMaxHelpers;
+      k = pend ? 0 : 64;
     } else {
       // lane r < nF learns the lane of the r-th pending path (a permutation of
       // all 64 lanes: pending lanes in order, then the others)
@@ -1609,7 +1617,7 @@ SRR_D int coop_mixture(const SceneView& S, const DiffSetup& me, bool& pend, int&
       s = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(lcg >> 32), src) << 32) |
           (uint32_t)__shfl((int)(uint32_t)lcg, src);
     }
-    const bool active = k < kMaxHelpers && t0 + k < kMixtureGuard;
+    const bool active = k < cap && t0 + k < kMixtureGuard;
     V3 nd = v3(0.f);
     float pv = 0;
     if (active) {
@@ -1636,7 +1644,7 @@ SRR_D int coop_mixture(const SceneView& S, const DiffSetup& me, bool& pend, int&
       // owner: its first successful helper (k ascending), else its last one
       int win = lane, m = 0;
       if (pend) {
-        m = min(kMaxHelpers, (63 - rank) / nF + 1);
+        m = min(cap, (63 - rank) / nF + 1);
         m = min(m, kMixtureGuard - tries);
         int j = 0;
         while (j < m - 1 && !((ok >> (rank + j * nF)) & 1)) ++j;
@@ -2202,7 +2210,9 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
   Rng rng{};
   int depth = 0;
   uint32_t nrays = 0;
+  uint32_t n_iter = 0, max_rounds = 0;  // wave-iterations, most mixture rounds (SRR_WAVE_TIMES diagnostics)
   for (;;) {
+    ++n_iter;
     uint64_t tq = TIMED ? __builtin_amdgcn_s_memtime() : 0;
     // refill lanes whose path ended, from the wave's pool of path indices; the
     // pool is re-armed one chunk ahead (an atomic whose result is first read an
@@ -2338,6 +2348,7 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
         tp[6] += __builtin_amdgcn_s_memtime() - tc;
         tp[7] += rounds;
       }
+      max_rounds = max(max_rounds, (uint32_t)rounds);
     }
     if (diff) {  // the rest of scatter<FAM_DIFF>: scattering_pdf and the record
       float c = dot(d_n, unit_vector(d_dir));  // material.h:100-105, 134-138
@@ -2396,10 +2407,12 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
   unsigned long long tot = nrays;
   for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
   if (lane_id() == 0 && tot) atomicAdd(W.counters, tot);
-  if (W.wave_times && lane_id() == 0) {  // diagnostics: when this wave started and ran out of paths
+  if (W.wave_times && lane_id() == 0) {  // diagnostics: start, exit, world rays, wave-iterations
     const size_t wv = (size_t)(blockIdx.x * blockDim.x + threadIdx.x) / 64;
-    W.wave_times[2 * wv] = t_start;
-    W.wave_times[2 * wv + 1] = __builtin_amdgcn_s_memrealtime();
+    W.wave_times[4 * wv] = t_start;
+    W.wave_times[4 * wv + 1] = __builtin_amdgcn_s_memrealtime();
+    W.wave_times[4 * wv + 2] = tot;
+    W.wave_times[4 * wv + 3] = n_iter | ((unsigned long long)max_rounds << 32);
   }
 }
 

@@ -358,8 +358,8 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
   unsigned long long* wave_times = nullptr;
   const int n_waves = (r->pw_lanes + 63) / 64;
   if (want_wave_times) {
-    RCHK(hipMalloc((void**)&wave_times, 2 * (size_t)n_waves * sizeof(unsigned long long)));
-    RCHK(hipMemsetAsync(wave_times, 0, 2 * (size_t)n_waves * sizeof(unsigned long long), st));
+    RCHK(hipMalloc((void**)&wave_times, 4 * (size_t)n_waves * sizeof(unsigned long long)));
+    RCHK(hipMemsetAsync(wave_times, 0, 4 * (size_t)n_waves * sizeof(unsigned long long), st));
   }
   RCHK(hipEventRecord(r->ev_beg, st));
   double kernel_ms = 0;
@@ -401,20 +401,28 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
     RCHK(hipEventElapsedTime(&ms, r->lanes[0].ev_t0, r->lanes[0].ev_t1));
     kernel_ms += ms;
     if (wave_times) {  // realtime clock: 100 MHz (10 ns ticks)
-      std::vector<unsigned long long> wt(2 * (size_t)n_waves);
+      std::vector<unsigned long long> wt(4 * (size_t)n_waves);
       RCHK(hipMemcpy(wt.data(), wave_times, wt.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-      std::vector<double> ex;
+      std::vector<std::pair<double, int>> ex;
       unsigned long long t0 = ~0ull;
       for (int i = 0; i < n_waves; ++i)
-        if (wt[2 * i + 1]) t0 = std::min(t0, wt[2 * i]);
+        if (wt[4 * i + 1]) t0 = std::min(t0, wt[4 * i]);
       for (int i = 0; i < n_waves; ++i)
-        if (wt[2 * i + 1]) ex.push_back((wt[2 * i + 1] - t0) * 1e-5);  // ms
+        if (wt[4 * i + 1]) ex.push_back({(wt[4 * i + 1] - t0) * 1e-5, i});  // ms
       std::sort(ex.begin(), ex.end());
       if (!ex.empty()) {
-        auto q = [&](double f) { return ex[std::min(ex.size() - 1, (size_t)(f * ex.size()))]; };
+        auto q = [&](double f) { return ex[std::min(ex.size() - 1, (size_t)(f * ex.size()))].first; };
         fprintf(stderr, "k_paths wave exits (ms after the first wave start, %zu waves, kernel %.3f ms): "
-                "min %.3f p10 %.3f p50 %.3f p90 %.3f p99 %.3f max %.3f\n", ex.size(), ms, ex.front(), q(0.1), q(0.5),
-                q(0.9), q(0.99), ex.back());
+                "min %.3f p10 %.3f p50 %.3f p90 %.3f p99 %.3f max %.3f\n", ex.size(), ms, ex.front().first, q(0.1),
+                q(0.5), q(0.9), q(0.99), ex.back().first);
+        // per wave: start, exit, world rays, wave-iterations, most mixture rounds in one iteration
+        auto show = [&](const char* what, int i) {
+          fprintf(stderr, "  %s wave %d: start %.3f exit %.3f rays %llu iterations %llu max mixture rounds %llu\n", what,
+                  i, (wt[4 * i] - t0) * 1e-5, (wt[4 * i + 1] - t0) * 1e-5, wt[4 * i + 2], wt[4 * i + 3] & 0xffffffffull,
+                  wt[4 * i + 3] >> 32);
+        };
+        show("median", ex[ex.size() / 2].second);
+        for (size_t k = ex.size() - std::min<size_t>(4, ex.size()); k < ex.size(); ++k) show("late", ex[k].second);
       }
       RCHK(hipMemsetAsync(wave_times, 0, wt.size() * sizeof(unsigned long long), st));
     }
