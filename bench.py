@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--count-visits", action="store_true", help="diagnostic: count mesh box/triangle tests (slower)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--save-frame", default="",
+                    help="rank 0 saves the assembled frame of the last step (per-pixel means, .npy)")
     return ap.parse_args()
 
 
@@ -139,10 +141,22 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # frame-end exchange backend: "nccl" (= RCCL over xGMI, one GPU per rank) or
+    # "gloo" (host-staged gather; lets several ranks share one GPU, e.g. the
+    # 2-rank rehearsal of tests/test_bench_multirank.py on a one-GPU box)
+    backend = os.environ.get("SRR_DIST_BACKEND", "nccl")
+    if backend not in ("nccl", "gloo"):
+        raise SystemExit(f"SRR_DIST_BACKEND must be nccl or gloo, not {backend!r}")
+    n_dev = torch.cuda.device_count()  # counting devices does not initialise the GPU
+    dev_idx = local % max(n_dev, 1)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
+        else:
+            dist.init_process_group("gloo")
+    torch.cuda.set_device(dev_idx)
+    dev = torch.device("cuda", dev_idx)
+    host_reduce = world > 1 and backend == "gloo"
 
     dv = {"divs": a.divs} if a.divs else {}
     if a.divs and a.scene == "s1":
@@ -154,14 +168,16 @@ def main():
     sc, cfg = fac()
     nx, ny, spp = a.nx or cfg["nx"], a.ny or cfg["ny"], a.spp or cfg["spp"]
     text = sc.text()
-    rend = capi.Renderer(text, device=local)
+    rend = capi.Renderer(text, device=dev_idx)
     sh = dist_frame.plan_shard(nx, ny, spp, cfg["max_depth"], rank, world, plan=a.plan, tile=a.tile,
                                batch_paths=a.batch_paths, flags=capi.FLAG_COUNT_VISITS if a.count_visits else 0)
-    ex = dist_frame.FrameExchange(sh, dev, dist if world > 1 else None)
+    ex = dist_frame.FrameExchange(sh, dev, dist if world > 1 else None, host_staged=host_reduce)
+
+    frame = [None]
 
     def step():
         st = rend.render_device(sh.params, ex.local.data_ptr())
-        ex.finish()  # frame-end exchange (RCCL) + assembly on rank 0
+        frame[0] = ex.finish()  # frame-end exchange (RCCL gather) + assembly on rank 0
         return st
 
     def barrier():
@@ -185,7 +201,8 @@ def main():
         launches += st["trace_launches"]
     barrier()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed, float(rays), trace_ms], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed, float(rays), trace_ms], dtype=torch.float64,
+                     device="cpu" if host_reduce else dev)
     if world > 1:
         tmax = t[:1].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -195,7 +212,11 @@ def main():
         rays_total = float(tsum[0].item())
     else:
         rays_total = float(rays)
+    if rank == 0 and a.save_frame:
+        import numpy as np
+        np.save(a.save_frame, frame[0].cpu().numpy())
     if rank == 0:
+        coll = "RCCL" if backend == "nccl" else "host-staged gloo"
         counts_json = json.load(open(os.path.join(ROOT, "tests", "golden", "traversal_counts.json")))
         key = CONFIG_KEY[a.scene]
         default_divs = {"s2": 10, "s3": 10, "s3_metal": 10, "s4": 40, "s5": 40}.get(a.scene)
@@ -232,13 +253,15 @@ def main():
             "data": "synthetic (scene built in code: Cornell box + tessellated Utah teapot)",
             "config": {"workload": f"{key}: {a.scene}{f' divs {a.divs}' if a.divs else ''} {nx}x{ny} {spp}spp "
                                    f"maxDepth {cfg['max_depth']}" + (
-                                   f", {a.tile}x{a.tile} tiles round-robin over {world} GPU(s), RCCL gather to rank 0 at frame end"
+                                   (f", {a.tile}x{a.tile} tiles round-robin over {world} GPUs, one {coll} gather "
+                                    f"to rank 0 at frame end" if world > 1 else
+                                    ", whole frame on one GPU (no collective)")
                                    if a.plan == "tiles" else
-                                   f" per GPU; {world} GPU(s) render sample ranges of one {spp * world}spp frame, "
-                                   f"RCCL reduce at frame end"),
+                                   f" per GPU; {world} GPU(s) render sample ranges of one {spp * world}spp frame" +
+                                   (f", one {coll} reduce at frame end" if world > 1 else "")),
                        "nx": nx, "ny": ny, "spp_per_gpu" if a.plan == "samples" else "spp": spp,
                        "frame_spp": sh.total_spp, "world_rays_per_step": int(rays_total / a.steps),
-                       "parallelism": f"{a.plan}{world}"},
+                       "parallelism": f"{a.plan}{world}", "dist_backend": backend if world > 1 else None},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                          "traffic": traffic, "kernel": kernel_name, "B_cfg": round(b_cfg, 1),

@@ -182,6 +182,8 @@ typedef struct srr_stats {
   int64_t stack_overflows; /* rays re-walked on the stackless BVH2             */
   int64_t deep_traversals; /* path engine: mesh traversals whose stack went past */
                            /* its LDS part into the global extension           */
+  int64_t mixture_capped;  /* path engine: resampling loops (Raytracing_n.cpp:79-83) */
+                           /* stopped by the 100,000-attempt cap   */
 } srr_stats;
 
 /* Flatten the scene and upload it to HIP device `device`. */

@@ -106,7 +106,7 @@ inline double drand48() { return R.drand(); }
 
 // Traversal counters (SURVEY §8(d) N_node / N_tri / N_prim), per thread; only
 // work done inside world->hit counts (light-pdf probes are excluded).
-struct Counters { long long world = 0, node = 0, tri = 0, prim = 0; };
+struct Counters { long long world = 0, node = 0, tri = 0, prim = 0, capped = 0; };
 thread_local Counters C;
 thread_local bool in_world = false;
 #define COUNT(f) do { if (in_world) ++C.f; } while (0)
@@ -1187,6 +1187,8 @@ struct Scene {
   const List* lights = nullptr;
 };
 
+constexpr int kMixtureGuard = 100000;  // attempts of one resampling loop (build definition)
+
 // Raytracing_n.cpp:55-106 -- recursive; `depth` is shared down the recursion.
 V color(const Scene& S, const Ray& r, int* depth, int max_depth) {
   Hit h;
@@ -1210,10 +1212,18 @@ V color(const Scene& S, const Ray& r, int* depth, int max_depth) {
         pl.p = S.lights;
         pl.o = h.p;
         MixturePdf p(&pl, s.pdf.get());
-        while (pdf_val == 0) {
+        // Raytracing_n.cpp:79-83 loops without bound; a hit point in a light's own
+        // plane never leaves it (every light sample runs parallel to the light, and
+        // the BSDF half is 0, Q1).  Build definition, shared with the
+        // product (kernels.hip kMixtureGuard): stop after kMixtureGuard attempts and
+        // keep the last one (pdf_val 0).
+        int attempts = 0;
+        while (pdf_val == 0 && attempts < kMixtureGuard) {
           scattered = Ray(h.p, p.generate(r.B), r.tm);
           pdf_val = p.value(r.B, scattered.B);
+          ++attempts;
         }
+        if (pdf_val == 0) ++C.capped;
       } else {
         scattered = Ray(h.p, s.pdf->generate(r.B), r.tm);
         pdf_val = s.pdf->value(r.B, scattered.B);
@@ -1490,8 +1500,9 @@ const char* oracle_last_error() { return orc::g_err.c_str(); }
 // pixels when pixels == NULL -- with per-path reseeding.  Outputs (any may be
 // NULL): paths[n_pix*ns*3] raw color() per path (before de_nan), rays[n_pix*ns]
 // world rays per path, img[n_pix*3] = mean of de_nan'd samples (before sqrt),
-// img8[n_pix*3] tone-mapped (Raytracing_n.cpp:848-867).  stats[4] = world rays,
-// box tests, triangle tests, analytic primitive tests.
+// img8[n_pix*3] tone-mapped (Raytracing_n.cpp:848-867).  stats[5] = world rays,
+// box tests, triangle tests, analytic primitive tests, resampling loops stopped
+// by the attempt cap (kMixtureGuard).
 int oracle_render(const char* scene_text, int nx, int ny, int ns, int max_depth, const int* pixels, int n_pixels,
                   float* paths, unsigned char* rays, float* img, unsigned char* img8, long long* stats,
                   int n_threads) {
@@ -1541,8 +1552,10 @@ int oracle_render(const char* scene_text, int nx, int ny, int ns, int max_depth,
     work(0);
     for (auto& t : th) t.join();
     if (stats) {
-      stats[0] = stats[1] = stats[2] = stats[3] = 0;
-      for (auto& c : cnt) { stats[0] += c.world; stats[1] += c.node; stats[2] += c.tri; stats[3] += c.prim; }
+      stats[0] = stats[1] = stats[2] = stats[3] = stats[4] = 0;
+      for (auto& c : cnt) {
+        stats[0] += c.world; stats[1] += c.node; stats[2] += c.tri; stats[3] += c.prim; stats[4] += c.capped;
+      }
     }
     return 0;
   } catch (const std::exception& e) {

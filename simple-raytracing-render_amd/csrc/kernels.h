@@ -103,6 +103,7 @@ struct PathWork {
   int2* gstack;           // the stack's global extension [gstack_cap][lanes] (deep meshes), or nullptr
   int gstack_cap;
   unsigned long long* wave_times;  // diagnostics (SRR_WAVE_TIMES): per wave [start, exit] s_memrealtime, or nullptr
+  int deep_tries;         // coop_mixture: failed attempts after which a path takes every free lane (32)
 };
 #ifndef SRR_KSTACK
 #define SRR_KSTACK 8

@@ -1029,6 +1029,13 @@ SRR_D void store_hit(const SceneView& S, const PathState& P, int p, const WorldH
 }
 
 // ================================================================ shading
+// Attempts of one resampling loop `while (pdf_val == 0)` (Raytracing_n.cpp:79-83).
+// The reference loops without bound, and a hit point in a light's own plane never
+// leaves the loop (every light sample runs parallel to the light, the BSDF half is
+// 0).  Build definition, shared with the oracle
+// (oracle/restate.cpp kMixtureGuard): stop after kMixtureGuard attempts and keep
+// the last attempt (pdf 0; the record's division then gives inf/NaN, de_nan'd).
+constexpr int kMixtureGuard = 100000;
 SRR_D V3 tex_value_slow(const SceneView& S, int ti, float u, float v, V3 p) {
   // checker_texture recursion (texture.h:13-19) unrolled to a few levels
   for (int guard = 0; guard < 8; ++guard) {
@@ -1559,7 +1566,7 @@ SRR_D uint64_t skip_attempt(const SceneView& S, uint64_t s) {
   return s;
 }
 
-constexpr int kMixtureGuard = 100000;  // the sequential loop's attempt cap (scatter)
+
 #ifndef SRR_COOP_HELPERS
 #define SRR_COOP_HELPERS 8
 #endif
@@ -1567,18 +1574,16 @@ constexpr int kMixtureGuard = 100000;  // the sequential loop's attempt cap (sca
 #define SRR_COOP_ID0 0
 #endif
 constexpr int kMaxHelpers = SRR_COOP_HELPERS;  // attempts of one path per round
-#ifndef SRR_DEEP_TRIES
-#define SRR_DEEP_TRIES 32
-#endif
-constexpr int kDeepTries = SRR_DEEP_TRIES;  // past this many failed attempts a path takes every free lane
 
 // Runs to completion the loops of every lane with `pend` (converged wave, all 64
 // lanes active).  In: the lane's setup, its LCG state before attempt `tries`.
 // Out: ndir, pdf and the LCG state after the first attempt with pdf != 0 (or the
 // guard's last attempt).  The first round is each pending lane's own attempt
 // (no exchange); later rounds spread the remaining paths over all 64 lanes.
+// deep_tries: past this many failed attempts a path takes every free lane
+// (PathWork::deep_tries, 32; SRR_DEEP_TRIES=0 forces it from the first round).
 SRR_D int coop_mixture(const SceneView& S, const DiffSetup& me, bool& pend, int& tries, uint64_t& lcg, V3& ndir,
-                       float& pdf) {
+                       float& pdf, int deep_tries) {
   int rounds = 0;
   const int lane = lane_id();
   const uint64_t lt = (1ull << lane) - 1;
@@ -1589,7 +1594,7 @@ SRR_D int coop_mixture(const SceneView& S, const DiffSetup& me, bool& pend, int&
     // paths whose loop has failed kDeepTries times (e.g. a hit point in the light's
     // own plane: every light sample runs parallel to it) may need up to the guard's
     // 100,000 attempts; once every pending path is that deep, all 64 lanes help
-    const int cap = __ballot(pend && tries < kDeepTries) == 0 ? 64 : kMaxHelpers;
+    const int cap = __ballot(pend && tries < deep_tries) == 0 ? 64 : kMaxHelpers;
     const int rank = pend ? __popcll(F & lt) : nF + __popcll(~F & lt);
     DiffSetup d;
     int t0, k;
@@ -2079,7 +2084,7 @@ SRR_D void scatter(const SceneView& S, const DMat& M, V3 rdir, float rtime, V3 h
     float pdf_val = 0;
     if (S.n_lights > 0) {
       (void)drand(rng);  // mixture_pdf ctor (pdf.h:175)
-      for (int guard = 0; pdf_val == 0 && guard < 100000; ++guard) {
+      for (int guard = 0; pdf_val == 0 && guard < kMixtureGuard; ++guard) {
         if (drand(rng) < 0.5) ndir = lights_random(S, hpt, rng);
         else ndir = bsdf_generate<F == FAM_BECK>(f, rdir, rng);
         pdf_val = 0.5 * lights_pdf(S, hpt, ndir) + 0.5 * bsdf_value<F == FAM_BECK>(f, rdir, ndir);
@@ -2210,6 +2215,7 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
   Rng rng{};
   int depth = 0;
   uint32_t nrays = 0;
+  uint32_t n_capped = 0;  // resampling loops stopped by kMixtureGuard
   uint32_t n_iter = 0, max_rounds = 0;  // wave-iterations, most mixture rounds (SRR_WAVE_TIMES diagnostics)
   for (;;) {
     ++n_iter;
@@ -2327,6 +2333,7 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
           else scatter<FAM_SPEC>(S, M, r.d, r.tm, h.p, h.n, h.u, h.v, rng, rec, sp, nd, nt);
           if (depth >= W.max_depth || slot >= W.lanes) atomicOr(W.err, 2);
           else rec_store(&W.rec[(size_t)depth * W.lanes + slot], rec);
+          if (!sp && S.n_lights > 0 && rec.w == 0) ++n_capped;  // the loop reached kMixtureGuard
           r = Ray{h.p, nd, nt};
           ++depth;
           done = false;
@@ -2342,7 +2349,7 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
         rounds = skip_mixture(S, ds, d_dead, pend, d_tries, rng.lcg, d_dir, d_pdf);
       } else {
         if (SRR_MIXTURE_SKIP == 2) rounds = skip_mixture(S, ds, d_dead, pend, d_tries, rng.lcg, d_dir, d_pdf, 1);
-        if (__ballot(pend)) rounds += coop_mixture(S, ds, pend, d_tries, rng.lcg, d_dir, d_pdf);
+        if (__ballot(pend)) rounds += coop_mixture(S, ds, pend, d_tries, rng.lcg, d_dir, d_pdf, W.deep_tries);
       }
       if (TIMED) {
         tp[6] += __builtin_amdgcn_s_memtime() - tc;
@@ -2351,6 +2358,7 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
       max_rounds = max(max_rounds, (uint32_t)rounds);
     }
     if (diff) {  // the rest of scatter<FAM_DIFF>: scattering_pdf and the record
+      if (d_pdf == 0) ++n_capped;  // the loop reached kMixtureGuard
       float c = dot(d_n, unit_vector(d_dir));  // material.h:100-105, 134-138
       if (c < 0) c = 0;
       const V3 as = d_atten * (c / kPi);
@@ -2407,6 +2415,11 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
   unsigned long long tot = nrays;
   for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
   if (lane_id() == 0 && tot) atomicAdd(W.counters, tot);
+  if (__ballot(n_capped != 0)) {
+    unsigned long long cap = n_capped;
+    for (int o = 32; o > 0; o >>= 1) cap += __shfl_xor(cap, o);
+    if (lane_id() == 0) atomicAdd(W.counters + 15, cap);
+  }
   if (W.wave_times && lane_id() == 0) {  // diagnostics: start, exit, world rays, wave-iterations
     const size_t wv = (size_t)(blockIdx.x * blockDim.x + threadIdx.x) / 64;
     W.wave_times[4 * wv] = t_start;

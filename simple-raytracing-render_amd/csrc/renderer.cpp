@@ -246,6 +246,10 @@ static hipError_t stage_pixels(srr_renderer* r, const int32_t* pix, int64_t npix
     r->pixels = nullptr;
     r->acc = nullptr;
     r->pix_cap = 0;
+    // the running sums went with the old buffer: nothing may continue them
+    r->acc_npix = 0;
+    r->acc_samples = 0;
+    std::fill(r->acc_key, r->acc_key + 5, -1);
     hipError_t e = hipMalloc((void**)&r->pixels, npix * sizeof(int32_t));
     if (e == hipSuccess) e = hipMalloc((void**)&r->acc, 3 * npix * sizeof(float));
     if (e != hipSuccess) return e;
@@ -357,10 +361,15 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
   static const bool want_wave_times = getenv("SRR_WAVE_TIMES") != nullptr;
   unsigned long long* wave_times = nullptr;
   const int n_waves = (r->pw_lanes + 63) / 64;
-  if (want_wave_times) {
-    RCHK(hipMalloc((void**)&wave_times, 4 * (size_t)n_waves * sizeof(unsigned long long)));
+  if (want_wave_times) {  // owned by the renderer (freed in ~srr_renderer), so no early return leaks it
+    if (!r->pw_wave_times) RCHK(hipMalloc((void**)&r->pw_wave_times, 4 * (size_t)n_waves * sizeof(unsigned long long)));
+    wave_times = r->pw_wave_times;
     RCHK(hipMemsetAsync(wave_times, 0, 4 * (size_t)n_waves * sizeof(unsigned long long), st));
   }
+  // attempts after which a pending resampling loop takes every free lane of its
+  // wave (kernels.hip coop_mixture); SRR_DEEP_TRIES=0 forces that branch (tests)
+  const char* dt_env = getenv("SRR_DEEP_TRIES");
+  const int deep_tries = dt_env ? std::max(0, atoi(dt_env)) : 32;
   RCHK(hipEventRecord(r->ev_beg, st));
   double kernel_ms = 0;
   for (int s0 = 0; s0 < p->spp; s0 += W) {
@@ -391,6 +400,7 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
     w.gstack = gst_cap ? r->pw_gstack : nullptr;
     w.gstack_cap = gst_cap;
     w.wave_times = wave_times;
+    w.deep_tries = deep_tries;
     RCHK(hipMemsetAsync(w.cursor, 0, sizeof(unsigned long long), st));
     RCHK(hipEventRecord(r->lanes[0].ev_t0, st));
     launch_paths(r->view, w, all_fam ? 1 : 0, st);
@@ -436,7 +446,6 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
   RCHK(hipEventRecord(r->ev_end, st));
   RCHK(hipStreamSynchronize(st));
   RCHK(hipGetLastError());
-  if (wave_times) (void)hipFree(wave_times);
   unsigned long long ctr[16] = {0};
   RCHK(hipMemcpy(ctr, r->pw_ctr, sizeof(ctr), hipMemcpyDeviceToHost));
   if (getenv("SRR_PATHS_TIMING") && ctr[9]) {
@@ -457,6 +466,7 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
   s.world_rays = (int64_t)rays;
   s.stack_overflows = (int64_t)ctr[11];
   s.deep_traversals = (int64_t)ctr[12];
+  s.mixture_capped = (int64_t)ctr[15];
   s.paths = npix * p->spp;
   s.trace_ms = kernel_ms;
   s.total_ms = total;
@@ -723,6 +733,7 @@ srr_renderer::~srr_renderer() {
   (void)hipFree(pw_raw);
   (void)hipFree(pw_rays);
   (void)hipFree(pw_ctr);
+  (void)hipFree(pw_wave_times);
   for (auto& L : lanes) {
     srr::free_lane_paths(L);
     (void)hipFree(L.cnt);

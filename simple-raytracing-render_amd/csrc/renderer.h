@@ -76,6 +76,7 @@ struct srr_renderer {
   uint8_t* pw_rays = nullptr;
   size_t pw_sample_cap = 0;
   unsigned long long* pw_ctr = nullptr;  // [0] world rays, [1] path cursor
+  unsigned long long* pw_wave_times = nullptr;  // SRR_WAVE_TIMES diagnostics, 4 words per wave
   int32_t* pixels = nullptr;
   size_t pix_cap = 0;
   // the shard whose pixel list (srr_shard_pixels) the renderer holds: {nx, ny,

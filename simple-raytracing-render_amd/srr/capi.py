@@ -36,7 +36,8 @@ class Stats(ctypes.Structure):
     _fields_ = [("world_rays", ctypes.c_int64), ("paths", ctypes.c_int64), ("trace_launches", ctypes.c_int64),
                 ("trace_ms", ctypes.c_double), ("shade_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
                 ("bounces", ctypes.c_int64), ("box_tests", ctypes.c_int64), ("tri_tests", ctypes.c_int64),
-                ("stack_overflows", ctypes.c_int64), ("deep_traversals", ctypes.c_int64)]
+                ("stack_overflows", ctypes.c_int64), ("deep_traversals", ctypes.c_int64),
+                ("mixture_capped", ctypes.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

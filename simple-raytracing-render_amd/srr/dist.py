@@ -73,17 +73,25 @@ class FrameExchange:
     `local` is this rank's [n_max, 3] float32 tensor of per-pixel means
     (``tiles``; rows beyond its pixel count are ignored) or sample sums
     (``samples``).  `finish()` returns the assembled [nx*ny, 3] frame of means
-    on rank 0 (None elsewhere)."""
+    on rank 0 (None elsewhere).
 
-    def __init__(self, sh: Shard, device, dist=None):
+    host_staged: the collective runs on host copies (gloo, which has no gather
+    or reduce of device tensors), so several ranks may share one GPU; the
+    assembled frame is the same bits as over RCCL."""
+
+    def __init__(self, sh: Shard, device, dist=None, host_staged=False):
         import torch
         self.sh, self.dist, self.torch = sh, dist, torch
+        self.host_staged = bool(host_staged and dist is not None)
         nx, ny = sh.params.nx, sh.params.ny
         self.n_max = max(sh.counts)
         self.local = torch.zeros((self.n_max, 3), dtype=torch.float32, device=device)
         self.image = torch.zeros((nx * ny, 3), dtype=torch.float32, device=device)
+        xdev = "cpu" if self.host_staged else device  # where the collective's buffers live
+        self.xlocal = torch.zeros((self.n_max, 3), dtype=torch.float32, device=xdev) if self.host_staged else None
         if sh.plan == "tiles":
-            self.gathered = [torch.zeros_like(self.local) for _ in range(sh.world)] if sh.rank == 0 else None
+            self.gathered = ([torch.zeros((self.n_max, 3), dtype=torch.float32, device=xdev)
+                              for _ in range(sh.world)] if sh.rank == 0 else None)
             self.idx = [torch.from_numpy(shard_pixels_of(sh, k).astype(np.int64)).to(device)
                         for k in range(sh.world)]
         # the renderer's mean: sum * (float)(1.0 / (float)ns)  (kernels.hip k_finish)
@@ -95,15 +103,25 @@ class FrameExchange:
             if sh.world == 1:
                 self.image[self.idx[0]] = self.local[:sh.counts[0]]
                 return self.image
-            self.dist.gather(self.local, self.gathered, dst=0)  # one exchange over RCCL / xGMI
+            if self.host_staged:
+                self.xlocal.copy_(self.local)
+                self.dist.gather(self.xlocal, self.gathered, dst=0)
+            else:
+                self.dist.gather(self.local, self.gathered, dst=0)  # one exchange over RCCL / xGMI
             if sh.rank != 0:
                 return None
             for k in range(sh.world):
-                self.image[self.idx[k]] = self.gathered[k][:sh.counts[k]]
+                self.image[self.idx[k]] = self.gathered[k][:sh.counts[k]].to(self.image.device)
             return self.image
         # samples: raw per-pixel sums of this rank's samples, reduced to rank 0
         if sh.world > 1:
-            self.dist.reduce(self.local, dst=0)
+            if self.host_staged:
+                self.xlocal.copy_(self.local)
+                self.dist.reduce(self.xlocal, dst=0)
+                if sh.rank == 0:
+                    self.local.copy_(self.xlocal)
+            else:
+                self.dist.reduce(self.local, dst=0)
             if sh.rank != 0:
                 return None
         torch.mul(self.local, self.inv_ns, out=self.image)

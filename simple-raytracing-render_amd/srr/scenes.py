@@ -130,6 +130,27 @@ def s6_mixed_lights() -> tuple[Scene, dict]:
     return sc, dict(nx=256, ny=256, spp=64, max_depth=50)
 
 
+def s7_coplanar_light() -> tuple[Scene, dict]:
+    """The resampling loop's attempt cap (DESIGN §2 build definitions): the
+    Cornell box (its ceiling light in the world) whose light list (hlist) holds
+    only a small triangle lying in the floor's plane y = 0 (where the barycentric
+    light samples of ``triangle::random`` stay exactly in the plane).  From a
+    floor hit point at y >= 0 every light sample runs in (or just below) the
+    triangle's plane, so ``triangle::hit`` rejects it (det < 1e-4,
+    triangle.h:146-148) and the lambertian value of that direction is 0
+    (pdf.h:40-45); BSDF samples have a zero value too (Q1) and meet the triangle's
+    plane at the hit point itself, outside the triangle.  The reference's
+    ``while (pdf_val == 0)`` (Raytracing_n.cpp:79-83) never ends there; srr and
+    the restatement stop after 100,000 attempts."""
+    sc = Scene()
+    objs, _ = _cornell(sc)
+    sc.set_world(sc.hitable_list(objs))
+    sc.camera((278, 278, -800), (278, 278, 0), (0, 1, 0), 40.0, 1.0, 0.0, 10.0, 0.0, 1.0)
+    tri_p = ((500, 0, 500), (500.5, 0, 500), (500.25, 0, 500.5))
+    sc.set_lights(sc.hitable_list([sc.triangle(*tri_p)]))
+    return sc, dict(nx=12, ny=12, spp=2, max_depth=50)
+
+
 SCENES = {
     "s1": s1_cornell,
     "s2": s2_cornell_teapot,
@@ -138,4 +159,5 @@ SCENES = {
     "s4": s4_soldier_standin,
     "s5": s5_soldier_fog,
     "s6": s6_mixed_lights,
+    "s7": s7_coplanar_light,
 }

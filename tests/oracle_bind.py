@@ -41,14 +41,17 @@ def _p(a):
 
 def render(scene_text: str, nx: int, ny: int, spp: int, max_depth: int = 50, pixels=None, threads: int = 1,
            want_paths: bool = True):
-    """Returns dict(paths[n,spp,3], rays[n,spp], img[n,3], img8[n,3], stats[4])."""
+    """Returns dict(paths[n,spp,3], rays[n,spp], img[n,3], img8[n,3], stats[5]).
+
+    stats: world rays, box tests, triangle tests, analytic primitive tests,
+    resampling loops stopped by the attempt cap."""
     n = nx * ny if pixels is None else len(pixels)
     pix = None if pixels is None else np.ascontiguousarray(pixels, dtype=np.int32)
     paths = np.zeros((n, spp, 3), np.float32) if want_paths else None
     rays = np.zeros((n, spp), np.uint8)
     img = np.zeros((n, 3), np.float32)
     img8 = np.zeros((n, 3), np.uint8)
-    stats = np.zeros(4, np.int64)
+    stats = np.zeros(5, np.int64)
     rc = lib().oracle_render(scene_text.encode(), nx, ny, spp, max_depth, _p(pix), n, _p(paths), _p(rays), _p(img),
                              _p(img8), _p(stats), threads)
     if rc != 0:

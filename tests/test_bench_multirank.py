@@ -1,0 +1,67 @@
+"""bench.py's N>1 path executed for real (VERDICT r2 missing #1): two ranks
+under torch.distributed.run, both on the one leased GPU, with the host-staged
+gloo exchange (SRR_DIST_BACKEND=gloo; RCCL needs one GPU per rank).  The
+render, the per-rank renderer and shard bookkeeping, the gather, rank 0's
+assembly and the max/sum timing reductions are bench.py's own code; only the
+collective's transport differs from the 8-GPU RCCL run.
+
+The assembled 2-rank frame must be bitwise the 1-rank frame, and the JSON line
+must report n_gpus 2, strong scaling and the frame's world rays (the sum over
+ranks equals the one-GPU count)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+ARGS = ["--steps", "2", "--warmup", "1", "--scene", "s2", "--nx", "96", "--ny", "80", "--spp", "16",
+        "--no-cpu-baseline"]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _json_line(out):
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert lines, out
+    return json.loads(lines[-1])
+
+
+@pytest.mark.parametrize("plan", ["tiles", "samples"])
+def test_bench_two_ranks_on_one_gpu(plan, tmp_path):
+    env = dict(os.environ, SRR_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    f1, f2 = str(tmp_path / "f1.npy"), str(tmp_path / "f2.npy")
+    one = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--plan", plan,
+                          *ARGS, "--save-frame", f1], capture_output=True, text=True, timeout=300, env=env,
+                         cwd=ROOT)
+    assert one.returncode == 0, one.stderr[-3000:]
+    two = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                          os.path.join(ROOT, "bench.py"), "--gpus", "2", "--plan", plan, *ARGS,
+                          "--save-frame", f2], capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert two.returncode == 0, two.stderr[-3000:]
+    j1, j2 = _json_line(one.stdout), _json_line(two.stdout)
+    print(plan, "1 rank:", j1["value"], j1["config"]["world_rays_per_step"], "2 ranks:", j2["value"],
+          j2["config"]["world_rays_per_step"], j2["config"]["workload"])
+    assert j2["n_gpus"] == 2 and j1["n_gpus"] == 1
+    img1, img2 = np.load(f1), np.load(f2)
+    if plan == "tiles":
+        assert j2["scaling"] == "strong"
+        # the same frame split over two ranks: the same world rays, the same bits
+        assert j2["config"]["world_rays_per_step"] == j1["config"]["world_rays_per_step"]
+        np.testing.assert_array_equal(img2.view(np.uint32), img1.view(np.uint32))
+    else:
+        assert j2["scaling"] == "weak"
+        assert j2["config"]["frame_spp"] == 2 * j1["config"]["frame_spp"]
+        assert img2.shape == img1.shape and np.isfinite(img2).all()
+    assert j2["config"]["dist_backend"] == "gloo"
+    assert j2["value"] > 0

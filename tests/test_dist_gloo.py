@@ -29,12 +29,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _rank_main(rank, world, port, plan, text, outdir):
+def _rank_main(rank, world, port, plan, text, outdir, staged=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         sh = dist_frame.plan_shard(NX, NY, SPP, 50, rank, world, plan=plan, tile=16)
-        ex = dist_frame.FrameExchange(sh, torch.device("cpu"), dist)
+        ex = dist_frame.FrameExchange(sh, torch.device("cpu"), dist, host_staged=staged)
         if plan == "tiles":
             r = ob.render(text, NX, NY, SPP, 50, pixels=sh.pixels, want_paths=False)
             ex.local[:sh.pixels.size] = torch.from_numpy(r["img"])
@@ -52,12 +52,14 @@ def _rank_main(rank, world, port, plan, text, outdir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("plan,world", [("tiles", 2), ("tiles", 3), ("samples", 2)])
-def test_multi_rank_frame_matches_single_render(plan, world, tmp_path):
+@pytest.mark.parametrize("plan,world,staged", [("tiles", 2, False), ("tiles", 3, False), ("samples", 2, False),
+                                               ("tiles", 2, True), ("samples", 2, True)])
+def test_multi_rank_frame_matches_single_render(plan, world, staged, tmp_path):
     """tiles: the gathered frame is bitwise the one-renderer frame; samples: the
-    reduced raw sums give the world*spp frame up to summation order."""
+    reduced raw sums give the world*spp frame up to summation order.  staged:
+    the host-staged exchange bench.py uses with SRR_DIST_BACKEND=gloo."""
     text = _scene_text()
-    mp.spawn(_rank_main, args=(world, _free_port(), plan, text, str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_rank_main, args=(world, _free_port(), plan, text, str(tmp_path), staged), nprocs=world, join=True)
     img = np.load(tmp_path / f"{plan}.npy")
     if plan == "tiles":
         ref = ob.render(text, NX, NY, SPP, 50, want_paths=False)["img"]

@@ -28,11 +28,15 @@ def _save_diag(name, bad, out):
                         rays=out["rays"][bad], mean=out["mean"][bad])
 
 
-@pytest.mark.parametrize("quad", ["0", "1"])
-def test_c2_full_frame_is_the_reference_frame(quad, monkeypatch):
-    """quad=1 forces the quad-cooperative mesh traversal (kernels.hip
-    mesh_hit4_quad) onto the L2-resident teapot, which by default runs per lane."""
-    monkeypatch.setenv("SRR_QUAD", quad)
+@pytest.mark.parametrize("mode", ["default", "quad", "deep0"])
+def test_c2_full_frame_is_the_reference_frame(mode, monkeypatch):
+    """quad forces the quad-cooperative mesh traversal (kernels.hip
+    mesh_hit4_quad) onto the L2-resident teapot, which by default runs per lane;
+    deep0 (SRR_DEEP_TRIES=0) sends every resampling loop to coop_mixture's
+    all-64-lanes branch from its first cooperative round."""
+    monkeypatch.setenv("SRR_QUAD", "1" if mode == "quad" else "0")
+    if mode == "deep0":
+        monkeypatch.setenv("SRR_DEEP_TRIES", "0")
     name = "c2_full"
     m = fullframe.meta(name)
     want = fullframe.load(name)
