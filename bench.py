@@ -43,9 +43,12 @@ def parse():
     ap.add_argument("--ny", type=int, default=0)
     ap.add_argument("--spp", type=int, default=0)
     ap.add_argument("--batch-paths", type=int, default=0)
-    ap.add_argument("--tile", type=int, default=16,
-                    help="tile edge of the tiles plan: 16 measured better balanced than 32 at 4 and 8 GPUs "
-                         "(tools/shard_balance.py, profiles/r02/shard_balance_*.json)")
+    ap.add_argument("--tile", type=int, default=1,
+                    help="tile edge of the tiles plan.  1 (pixels dealt round-robin, each row rotated by one) "
+                         "balances the shards' COST, not just their rays: 8 C2 shards within 0.5 %% of their "
+                         "mean time vs 10 %% at 16x16 and 12 %% at 32x32 (tools/shard_balance.py, "
+                         "profiles/r03/shard_balance_*.json); a wave renders samples of one pixel, so smaller "
+                         "tiles cost no coherence")
     ap.add_argument("--plan", default="tiles", choices=["tiles", "samples"],
                     help="multi-GPU split: tiles = strong scaling, the north_star split (one frame, --tile tiles "
                          "round-robin, one gather to rank 0; bitwise the 1-GPU image), samples = weak scaling "

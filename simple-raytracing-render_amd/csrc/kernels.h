@@ -23,6 +23,7 @@ struct SceneView {  // device pointers into the flattened tables (device_scene.h
   int node4_lds;        // leading nodes the path kernel keeps in LDS (<= kPathsLdsNodes)
   int quad_trace;       // k_paths traces meshes quad-cooperatively (BVH4 larger than an XCD's L2)
   int quad_max;         // ...when at most this many lanes of the wave enter the mesh (else per lane)
+  int mesh_obj;         // the world list's one top-level mesh object (k_paths CMP variant), else -1
   const float4* tri_pos;  // 4 float4 per triangle: p0, p1, p2, pad
   const TriShade* tri_shade;
   const DMedium* media;
@@ -104,6 +105,9 @@ struct PathWork {
   int gstack_cap;
   unsigned long long* wave_times;  // diagnostics (SRR_WAVE_TIMES): per wave [start, exit] s_memrealtime, or nullptr
   int deep_tries;         // coop_mixture: failed attempts after which a path takes every free lane (32)
+  int dbg;                // A/B diagnostics (SRR_PATHS_DBG), 0 in production
+  float* slow_rays;       // diagnostics build (-DSRR_SLOW_RAYS=ticks): [65536][16] records of slow world hits
+  unsigned* slow_count;
 };
 #ifndef SRR_KSTACK
 #define SRR_KSTACK 8
@@ -134,7 +138,11 @@ int launch_kat(int kind, int n, int w, float* d_rec, const float* d_aux, const D
                const KatTables& kt);
 // MERL table lookup (merl.h) for n queries; device pointers
 int launch_merl_lookup(const double* table, int64_t n, const double* angles, double* rgb, int32_t* cell);
-void launch_accumulate_window(const float* sample, int npix, int spp_w, float* acc, hipStream_t st);
+// acc[pixel] (+)= the window's samples in order; init: acc starts at 0 (no
+// memset); out != nullptr (the last window): also out = acc * (float)(1.0 / scale_ns)
+// (k_finish), or the raw sums when scale_ns == 0
+void launch_accumulate_window(const float* sample, int npix, int spp_w, float* acc, hipStream_t st, bool init = false,
+                              float* out = nullptr, int scale_ns = 0);
 void launch_raygen(const SceneView& S, const PathState& P, const BatchInfo& B, hipStream_t st);
 void launch_trace(const SceneView& S, const PathState& P, const int* active, const int* count, int max_n,
                   int* lists, int list_cap, int* fam_count, int* fetch, int max_depth, unsigned long long* ctr,

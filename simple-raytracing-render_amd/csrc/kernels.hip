@@ -238,6 +238,9 @@ struct TraceCtx {
   // SRR_TIMING diagnostics (wave-uniform): cycles inside mesh traversals, steps
   mutable uint64_t mesh_cycles = 0;
   mutable int mesh_steps = 0;
+#ifdef SRR_SLOW_RAYS
+  mutable int last_steps = 0;  // diagnostics build: node steps | 1 << 30 on overflow, of this lane's last walk
+#endif
 };
 
 // Pruning margin: a subtree is skipped only when its box's UNCLIPPED entry
@@ -254,11 +257,89 @@ struct TraceCtx {
 // the mesh's own surface: 1,115 world rays of the 512x512x1024 C2 frame.)
 constexpr float kPruneSlack = 1.0625f;
 
+// A NaN t bound (tmax): the world list's closest-so-far goes NaN when an
+// earlier object reports a hit at t = NaN -- e.g. a ray lying in an xz_rect
+// light's plane, (k - o.y) / d.y = 0 / 0, which passes every comparison of
+// aarect.h:115-121.  aabb::hit then rejects no box (tmax stays NaN, and
+// `tmax <= tmin` is false, aabb.h:33-49), so the reference walks the whole BVH
+// and folds every triangle: the result is the fold over all triangles of the
+// mesh, which `wins` reproduces in any order.  Walking the tree here cost up
+// to 17 ms for one such ray (~2,000 node steps with the global stack, then
+// 6,400 triangle tests, every fetch dependent): it set the end of a tile shard
+// (profiles/r03/slow_rays_s2.txt).  Instead the wave's active lanes scan the
+// triangles together for each such ray and reduce by `wins`: the same
+// (found, t, triangle) as the walk, bit for bit.
+SRR_D void mesh_scan_nan(const SceneView& S, const DMesh& m, const Ray& r, bool is_medium, uint64_t nanm,
+                         bool& found, float& best_t, int& best_i) {
+  const uint64_t act = __ballot(true);
+  const int nact = __popcll(act);
+  const int me = __popcll(act & ((1ull << __lane_id()) - 1));
+  const int t_end = m.tri_off + m.n_tris;
+  while (nanm) {
+    const int L = __ffsll((unsigned long long)nanm) - 1;
+    nanm &= nanm - 1;
+    const V3 o = v3(__shfl(r.o.x, L), __shfl(r.o.y, L), __shfl(r.o.z, L));
+    const V3 d = v3(__shfl(r.d.x, L), __shfl(r.d.y, L), __shfl(r.d.z, L));
+    const V3 dir = d / length(d);
+    bool f = false;
+    float bt = 0;
+    int bi = -1;
+    for (int ti = m.tri_off + me; ti < t_end; ti += nact) {
+      const float4* tp = S.tri_pos + kTriStride * (size_t)ti;
+      const float4 a = tp[0], b = tp[1], c = tp[2];
+      const V3 p0 = v3(a.x, a.y, a.z), p1 = v3(b.x, b.y, b.z), p2 = v3(c.x, c.y, c.z);
+      float t, u, v;
+      bool h = tri_hit(p0, p1, p2, true, o, dir, t, u, v);
+      if (!h && is_medium) h = tri_hit(p0, p1, p2, false, o, dir, t, u, v);
+      if (h && (!f || wins(t, ti, bt, bi))) {
+        f = true;
+        bt = t;
+        bi = ti;
+      }
+    }
+    // reduce over the active lanes in lane order (wins is a strict total order
+    // on (t, index), so the order does not change the winner)
+    bool rf = false;
+    float rt = 0;
+    int ri = -1;
+    for (uint64_t a2 = act; a2; a2 &= a2 - 1) {
+      const int j = __ffsll((unsigned long long)a2) - 1;
+      const bool fj = __shfl((int)f, j) != 0;
+      const float tj = __shfl(bt, j);
+      const int ij = __shfl(bi, j);
+      if (fj && (!rf || wins(tj, ij, rt, ri))) {
+        rf = true;
+        rt = tj;
+        ri = ij;
+      }
+    }
+    if ((int)__lane_id() == L) {
+      found = rf;
+      best_t = rt;
+      best_i = ri;
+    }
+  }
+}
+
 // 4-wide traversal of one mesh; same result as mesh_hit (the reference's
 // leaf set, min t, ties to the later DFS triangle).
 template <bool PRUNE, bool TIMING = false>
 SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmin, float tmax, bool is_medium,
                      MeshHit& out, const TraceCtx& cx) {
+  if (const uint64_t nanm = __ballot(!(tmax == tmax))) {  // NaN bound: the fold over all triangles
+    bool f = false;
+    float bt = 0;
+    int bi = -1;
+    mesh_scan_nan(S, m, r, is_medium, nanm, f, bt, bi);
+    if (!(tmax == tmax)) {
+#ifdef SRR_SLOW_RAYS
+      cx.last_steps |= 1 << 28;  // diagnostics build: this lane took the NaN-bound scan
+#endif
+      out.t = bt;
+      out.tri = bi;
+      return f;
+    }
+  }
   const V3 inv = v3(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
   const float len = length(r.d);
   const V3 dir = r.d / len;
@@ -410,6 +491,9 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
     const uint64_t dm = __ballot(deep);
     if (dm && (int)__lane_id() == __ffsll((unsigned long long)dm) - 1) atomicAdd(cx.ovf + 1, (unsigned long long)__popcll(dm));
   }
+#ifdef SRR_SLOW_RAYS
+  cx.last_steps += (int)(nbox / 4) | (overflow ? 1 << 30 : 0) | (deep ? 1 << 29 : 0);
+#endif
   if (overflow) {  // rare: exact re-walk
     if (cx.ovf) atomicAdd(cx.ovf, 1ull);
     return mesh_hit<false>(S, m, r, tmin, tmax, is_medium, out, cx.ctr);
@@ -456,6 +540,20 @@ SRR_D void quad_best(bool& f, float& t, int& i) {
 template <bool PRUNE>
 SRR_D bool mesh_hit4_quad(const SceneView& S, const DMesh& m, const Ray& r, float tmin, float tmax, bool is_medium,
                           MeshHit& out, const TraceCtx& cx) {
+  if (const uint64_t nanm = __ballot(!(tmax == tmax))) {  // NaN bound: the fold over all triangles (mesh_scan_nan)
+    bool f = false;
+    float bt = 0;
+    int bi = -1;
+    mesh_scan_nan(S, m, r, is_medium, nanm, f, bt, bi);
+    if (!(tmax == tmax)) {
+#ifdef SRR_SLOW_RAYS
+      cx.last_steps |= 1 << 28;  // diagnostics build: this lane took the NaN-bound scan
+#endif
+      out.t = bt;
+      out.tri = bi;
+      return f;
+    }
+  }
   const V3 inv = v3(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
   // every lane tests the mesh's root box -- the reference's bvh_node root, whose
   // own box test comes first in bvh.h:64-66 -- itself
@@ -861,6 +959,31 @@ struct WorldHit {
   int prim;
   float t;
 };
+
+// objects [k0, k1) of the world list, continuing a closest-so-far `closest`
+template <bool MEDIA, int TR>
+SRR_D void world_objs(const SceneView& S, const Ray& r, Rng& rng, const TraceCtx& cx, int k0, int k1, WorldHit& w,
+                      float& closest) {
+  const float tmin = 0.001f;
+  for (int k = k0; k < k1; ++k) {
+    const DObj ob = wload<TR>(S.objs, k);
+    Ray lr = chain_in<TR>(S, ob, r);
+    ObjHit h;
+    bool hit;
+    if (MEDIA && ob.kind == OBJ_MEDIUM) {
+      hit = medium_hit<TR>(S, wload<TR>(S.media, ob.idx), lr, tmin, closest, rng, h.t, cx);
+      h.prim = -1;
+    } else {
+      hit = basic_hit<TR>(S, ob, lr, tmin, closest, false, h, cx);
+    }
+    if (hit) {
+      closest = h.t;
+      w.obj = k;
+      w.prim = h.prim;
+      w.t = h.t;
+    }
+  }
+}
 
 template <bool MEDIA, int TR>
 SRR_D WorldHit world_hit(const SceneView& S, const Ray& r, Rng& rng, const TraceCtx& cx) {
@@ -2163,8 +2286,19 @@ SRR_D float4 rec_load(const float4* p) { return SRR_REC_NT ? ntl(p) : *p; }
 constexpr int kPathsBlock = 256;
 constexpr unsigned long long kPoolChunk = 64;  // path indices a wave takes per cursor atomic
 
-template <bool MEDIA, bool ALLFAM, int MINB, bool TIMED = false, bool WL = true, bool QUAD = false>
+// CMP: block-level compaction of the mesh traversal (scenes whose world list
+// holds one mesh at top level, SceneView::mesh_obj).  Each wave-iteration, every
+// lane tests the objects before the mesh and the mesh's root box (the
+// reference's bvh_node root, which contains every leaf box: a miss there is the
+// reference's miss, bvh.h:66); the block's lanes whose ray enters append it to
+// an LDS queue, the queue is traversed densely by the block's first lanes, and
+// each owner takes its result back and tests the objects after the mesh.  The
+// result of every ray is mesh_hit4's, so paths stay bit-identical.
+constexpr int kPathsLdsNodesCmp = 56;  // LDS node cache of the CMP variant (room for the queue)
+
+template <bool MEDIA, bool ALLFAM, int MINB, bool TIMED = false, bool WL = true, bool QUAD = false, bool CMP = false>
 __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathWork W) {
+  static_assert(!CMP || (!MEDIA && !TIMED && WL && !QUAD), "CMP: world list in LDS, no media, per-lane walks");
   // TIMED (diagnostics): per-wave cycles in refill / world hit (mesh part) / record+scatter / fold
   uint64_t tp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t it = 0;
@@ -2192,12 +2326,18 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
   }
   __shared__ int s_node[kStack * kPathsBlock];
   __shared__ float s_t[kStack * kPathsBlock];
-  __shared__ float4 s_n4[kPathsLdsNodes * 8];
-  for (int i = threadIdx.x; i < S0.node4_lds * 8; i += blockDim.x) s_n4[i] = S0.node4[i];
+  constexpr int kNodesLds = CMP ? kPathsLdsNodesCmp : kPathsLdsNodes;
+  const int n_lds_nodes = min(S0.node4_lds, kNodesLds);
+  __shared__ float4 s_n4[kNodesLds * 8];
+  for (int i = threadIdx.x; i < n_lds_nodes * 8; i += blockDim.x) s_n4[i] = S0.node4[i];
+  // CMP: the mesh-ray queue, SoA [8][kPathsBlock]: origin, direction, t bound
+  // (in) / hit t (out), triangle (out); per-wave queue counts | active bit
+  __shared__ float s_q[CMP ? 8 * kPathsBlock : 1];
+  __shared__ int s_wc[CMP ? kPathsBlock / 64 : 1];
   __syncthreads();
   TraceCtx cx{nullptr, to_lds(s_node + threadIdx.x), to_lds(s_t + threadIdx.x)};
   cx.lds_nodes = (const __attribute__((address_space(3))) f32x4*)to_lds(s_n4);
-  cx.lds_count = S0.node4_lds;
+  cx.lds_count = n_lds_nodes;
   cx.st_cap = W.stack_cap;
   cx.ovf = W.counters + 11;
   cx.gst = W.gstack;
@@ -2265,7 +2405,7 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
       if (lane_id() == 0) nxt_lane0 = (uint32_t)atomicAdd(W.cursor, (unsigned long long)kPoolChunk);
       nxt_armed = true;
     }
-    if (__ballot(g >= 0) == 0) break;
+    if (!CMP && __ballot(g >= 0) == 0) break;  // (CMP: the block leaves together, below)
     if (TIMED) {
       __builtin_amdgcn_s_waitcnt(0);
       const uint64_t t = __builtin_amdgcn_s_memtime();
@@ -2284,8 +2424,104 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
     float d_pdf = 0;
     int d_tries = 0;
     bool d_dead = false;
+    WorldHit w{-1, -1, 0};
+    if constexpr (CMP) {
+      const int mk = S0.mesh_obj;
+      const DObj mob = S.objs[mk];
+      const DMesh mm = S.meshes[mob.idx];
+      float closest = FLT_MAX;  // Raytracing_n.cpp:58
+      bool want = false;
+      Ray lr{};
+      if (g >= 0) {
+        world_objs<false, TR>(S, r, rng, cx, 0, mk, w, closest);
+        lr = chain_in<TR>(S, mob, r);
+        const V3 inv = v3(1.0f / lr.d.x, 1.0f / lr.d.y, 1.0f / lr.d.z);
+        // W.dbg (A/B diagnostics): bit 0 queues every ray (no root-box test);
+        // bit 1 walks in-lane (the variant's barriers without the compaction)
+        want = (W.dbg & 1) ? true : slab(S0.nodes[2 * mm.node_off], S0.nodes[2 * mm.node_off + 1], lr.o, inv, 0.001f, closest);
+        if (want && (W.dbg & 2)) {
+          MeshHit mh;
+          if (mesh_hit4<true>(S, mm, lr, 0.001f, closest, false, mh, cx)) {
+            closest = mh.t;
+            w = WorldHit{mk, mh.tri, closest};
+          }
+          want = false;
+        }
+      }
+      const uint64_t wm = __ballot(want);
+      const bool wave_busy = __ballot(g >= 0) != 0;  // (ballots outside the lane-0 branch: all lanes vote)
+      const int wv = threadIdx.x >> 6;
+      if (lane_id() == 0) s_wc[wv] = __popcll(wm) | (wave_busy ? 0x10000 : 0);
+      __syncthreads();
+      int base = 0, nq = 0, act = 0;
+#pragma unroll
+      for (int k = 0; k < kPathsBlock / 64; ++k) {
+        const int c = s_wc[k];
+        base += k < wv ? (c & 0xffff) : 0;
+        nq += c & 0xffff;
+        act |= c >> 16;
+      }
+      if (!act) break;  // every lane of the block is out of paths (block-uniform)
+      const int qi = base + __popcll(wm & ((1ull << lane_id()) - 1));
+      if (want) {
+        s_q[qi] = lr.o.x;
+        s_q[kPathsBlock + qi] = lr.o.y;
+        s_q[2 * kPathsBlock + qi] = lr.o.z;
+        s_q[3 * kPathsBlock + qi] = lr.d.x;
+        s_q[4 * kPathsBlock + qi] = lr.d.y;
+        s_q[5 * kPathsBlock + qi] = lr.d.z;
+        s_q[6 * kPathsBlock + qi] = closest;
+      }
+      __syncthreads();
+      if ((int)threadIdx.x < nq) {  // the queue, densely: waves 0 .. ceil(nq / 64) - 1
+        const int i = threadIdx.x;
+        const Ray qr{v3(s_q[i], s_q[kPathsBlock + i], s_q[2 * kPathsBlock + i]),
+                     v3(s_q[3 * kPathsBlock + i], s_q[4 * kPathsBlock + i], s_q[5 * kPathsBlock + i]), 0.f};
+        MeshHit mh;
+        const bool f = mesh_hit4<true>(S, mm, qr, 0.001f, s_q[6 * kPathsBlock + i], false, mh, cx);
+        s_q[6 * kPathsBlock + i] = mh.t;
+        s_q[7 * kPathsBlock + i] = __int_as_float(f ? mh.tri : -1);
+      }
+      __syncthreads();
+      if (want) {
+        const int tri = __float_as_int(s_q[7 * kPathsBlock + qi]);
+        if (tri >= 0) {
+          closest = s_q[6 * kPathsBlock + qi];
+          w = WorldHit{mk, tri, closest};
+        }
+      }
+      if (g >= 0) world_objs<false, TR>(S, r, rng, cx, mk + 1, S.n_world, w, closest);
+    }
     if (g >= 0) {
-      const WorldHit w = world_hit<MEDIA, TIMED ? (TR_BVH4_TIMED | (WL ? TR_WL : 0)) : TR>(S, r, rng, cx);
+#ifdef SRR_SLOW_RAYS
+      const uint64_t t_w0 = __builtin_amdgcn_s_memrealtime();
+      cx.last_steps = 0;
+      const Ray r_in = r;
+#endif
+      if constexpr (!CMP) w = world_hit<MEDIA, TIMED ? (TR_BVH4_TIMED | (WL ? TR_WL : 0)) : TR>(S, r, rng, cx);
+#ifdef SRR_SLOW_RAYS
+      // diagnostics build: every lane of a world hit slower than SRR_SLOW_RAYS
+      // ticks (100 MHz) records its ray: g, depth, o, d, time, ticks, steps, hit
+      const uint64_t t_w = __builtin_amdgcn_s_memrealtime() - t_w0;
+      if ((t_w > (uint64_t)SRR_SLOW_RAYS || (cx.last_steps & (1 << 28))) && W.slow_rays) {
+        const unsigned q = atomicAdd(W.slow_count, 1u);
+        if (q < 65536u) {
+          float* e = W.slow_rays + 16 * (size_t)q;
+          e[0] = __int_as_float(g);
+          e[1] = __int_as_float(depth);
+          e[2] = r_in.o.x; e[3] = r_in.o.y; e[4] = r_in.o.z;
+          e[5] = r_in.d.x; e[6] = r_in.d.y; e[7] = r_in.d.z;
+          e[8] = r_in.tm;
+          e[9] = __int_as_float((int)t_w);
+          e[10] = __int_as_float(cx.last_steps);
+          e[11] = __int_as_float(w.obj);
+          e[12] = __int_as_float(w.prim);
+          e[13] = w.t;
+          e[14] = __int_as_float(slot);
+          e[15] = __int_as_float((int)(t_w0 & 0x7fffffff));
+        }
+      }
+#endif
       if (TIMED) {
         const uint64_t t = __builtin_amdgcn_s_memtime();
         tp[1] += t - tq - cx.mesh_cycles;
@@ -2434,13 +2670,39 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
 // stages 256 pixels x 16 samples through LDS with coalesced loads, then each
 // thread adds its own pixel's samples in order.
 constexpr int kAccChunk = 16;
-__global__ void __launch_bounds__(256) k_accumulate_window(const float* sample, int npix, int spp_w, float* acc) {
+// init: the sums start from 0 (the frame's first window; no memset of acc).
+// out (the frame's last window, else nullptr): also writes the pixel's output --
+// the mean sum * (float)(1.0 / ns) of k_finish, or (scale_ns == 0) the raw sums.
+struct AccOut {
+  float* out;
+  int scale_ns;
+};
+SRR_D void acc_write(float* acc, AccOut o, size_t a, float cx, float cy, float cz) {
+  acc[a] = cx;
+  acc[a + 1] = cy;
+  acc[a + 2] = cz;
+  if (o.out) {
+    if (o.scale_ns) {
+      const float k = 1.0 / (float)o.scale_ns;  // k_finish
+      o.out[a] = cx * k;
+      o.out[a + 1] = cy * k;
+      o.out[a + 2] = cz * k;
+    } else {
+      o.out[a] = cx;
+      o.out[a + 1] = cy;
+      o.out[a + 2] = cz;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) k_accumulate_window(const float* sample, int npix, int spp_w, float* acc,
+                                                           int init, AccOut o) {
   __shared__ float tile[256 * (3 * kAccChunk + 1)];
   const int p0 = blockIdx.x * 256;
   const int lp = p0 + threadIdx.x;
   const int np = min(256, npix - p0);
   float cx = 0, cy = 0, cz = 0;
-  if (lp < npix) {
+  if (lp < npix && !init) {
     cx = acc[3 * (size_t)lp];
     cy = acc[3 * (size_t)lp + 1];
     cz = acc[3 * (size_t)lp + 2];
@@ -2463,23 +2725,21 @@ __global__ void __launch_bounds__(256) k_accumulate_window(const float* sample, 
     __syncthreads();
   }
   if (lp >= npix) return;
-  const size_t a = 3 * (size_t)lp;
-  acc[a] = cx;
-  acc[a + 1] = cy;
-  acc[a + 2] = cz;
+  acc_write(acc, o, 3 * (size_t)lp, cx, cy, cz);
 }
 
 // The same sums with 16-byte loads, for windows of a multiple of kAccChunk samples:
 // a pixel's chunk is 12 contiguous float4 (16-byte aligned), so a block fetches
 // its 256 x 16 samples with 12 float4 loads per thread (no per-element division).
-__global__ void __launch_bounds__(256) k_accumulate_window16(const float4* sample4, int npix, int spp_w, float* acc) {
+__global__ void __launch_bounds__(256) k_accumulate_window16(const float4* sample4, int npix, int spp_w, float* acc,
+                                                             int init, AccOut o) {
   __shared__ float tile[256 * (3 * kAccChunk + 1)];
   constexpr int kQ = 3 * kAccChunk / 4;  // float4 per pixel chunk
   const int p0 = blockIdx.x * 256;
   const int lp = p0 + threadIdx.x;
   const int np = min(256, npix - p0);
   float cx = 0, cy = 0, cz = 0;
-  if (lp < npix) {
+  if (lp < npix && !init) {
     cx = acc[3 * (size_t)lp];
     cy = acc[3 * (size_t)lp + 1];
     cz = acc[3 * (size_t)lp + 2];
@@ -2518,10 +2778,7 @@ __global__ void __launch_bounds__(256) k_accumulate_window16(const float4* sampl
       }
       __syncthreads();
     }
-    const size_t a = 3 * (size_t)lp;
-    acc[a] = cx;
-    acc[a + 1] = cy;
-    acc[a + 2] = cz;
+    acc_write(acc, o, 3 * (size_t)lp, cx, cy, cz);
     return;
   }
   for (int s0 = 0; s0 < spp_w; s0 += kAccChunk) {
@@ -2547,10 +2804,7 @@ __global__ void __launch_bounds__(256) k_accumulate_window16(const float4* sampl
     __syncthreads();
   }
   if (lp >= npix) return;
-  const size_t a = 3 * (size_t)lp;
-  acc[a] = cx;
-  acc[a + 1] = cy;
-  acc[a + 2] = cz;
+  acc_write(acc, o, 3 * (size_t)lp, cx, cy, cz);
 }
 
 constexpr int kMaxRegions = 8;
@@ -2954,7 +3208,7 @@ int paths_lanes_per_device(const SceneView& S, int device) {
   (void)S;
   int cus = 0, per_cu = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)dev::k_paths<false, false, 2>,
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)dev::k_paths<false, false, 4>,
                                                    dev::kPathsBlock, 0) != hipSuccess || per_cu <= 0)
     per_cu = 2;
   per_cu = std::max(per_cu, paths_min_blocks());
@@ -2979,10 +3233,18 @@ void launch_paths(const SceneView& S, const PathWork& W, int all_families, hipSt
 #undef SRR_LAUNCH_PATHS_G
     return;
   }
+  // opt-in (SRR_COMPACT=1): measured 20 % slower on C2
+  static const bool compact = [] {
+    const char* e = getenv("SRR_COMPACT");
+    return e && atoi(e) != 0;
+  }();
+  const bool cmp = compact && S.mesh_obj >= 0 && !S.has_media && !S.quad_trace && !timed;
 #define SRR_LAUNCH_PATHS(M, A, B)                                                                      \
   if (timed) hipLaunchKernelGGL((dev::k_paths<M, A, 4, true>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W); \
+  else if (!M && cmp && B == 4) hipLaunchKernelGGL((dev::k_paths<false, A, 4, false, true, false, true>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W); \
   else if (S.quad_trace && B == 4) hipLaunchKernelGGL((dev::k_paths<M, A, 4, false, true, true>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W); \
   else hipLaunchKernelGGL((dev::k_paths<M, A, B>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W)
+#ifdef SRR_OCC_VARIANTS  // occupancy A/B builds (SRR_PATHS_OCC): 2, 3, 5 and 6 blocks per CU
 #define SRR_LAUNCH_PATHS_B(M, A)                          \
   switch (paths_min_blocks()) {                           \
     case 2: SRR_LAUNCH_PATHS(M, A, 2); break;             \
@@ -2991,6 +3253,9 @@ void launch_paths(const SceneView& S, const PathWork& W, int all_families, hipSt
     case 6: SRR_LAUNCH_PATHS(M, A, 6); break;             \
     default: SRR_LAUNCH_PATHS(M, A, 4); break;            \
   }
+#else
+#define SRR_LAUNCH_PATHS_B(M, A) SRR_LAUNCH_PATHS(M, A, 4);
+#endif
   if (S.has_media) {
     if (all_families) { SRR_LAUNCH_PATHS_B(true, true) }
     else { SRR_LAUNCH_PATHS_B(true, false) }
@@ -3015,13 +3280,16 @@ int launch_kat(int kind, int n, int w, float* d_rec, const float* d_aux, const D
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-void launch_accumulate_window(const float* sample, int npix, int spp_w, float* acc, hipStream_t st) {
+void launch_accumulate_window(const float* sample, int npix, int spp_w, float* acc, hipStream_t st, bool init,
+                              float* out, int scale_ns) {
   static const bool scalar = getenv("SRR_ACC_SCALAR") != nullptr;  // A/B diagnostics
+  const dev::AccOut o{out, scale_ns};
   if (spp_w % dev::kAccChunk == 0 && ((uintptr_t)sample & 15) == 0 && !scalar)
     hipLaunchKernelGGL(dev::k_accumulate_window16, dim3((npix + 255) / 256), dim3(256), 0, st, (const float4*)sample,
-                       npix, spp_w, acc);
+                       npix, spp_w, acc, init ? 1 : 0, o);
   else
-    hipLaunchKernelGGL(dev::k_accumulate_window, dim3((npix + 255) / 256), dim3(256), 0, st, sample, npix, spp_w, acc);
+    hipLaunchKernelGGL(dev::k_accumulate_window, dim3((npix + 255) / 256), dim3(256), 0, st, sample, npix, spp_w, acc,
+                       init ? 1 : 0, o);
 }
 
 }  // namespace srr

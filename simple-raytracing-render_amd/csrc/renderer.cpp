@@ -113,6 +113,16 @@ int renderer_create(const Scene& sc, int device, srr_renderer** out, std::string
     const char* q = getenv("SRR_QUAD_MAX");
     V.quad_max = q ? atoi(q) : 32;  // 640k-tri teapot: 16 -> 1,569, 32 -> 1,598, 64 -> 1,552 Msamples/s
   }
+  {  // one mesh at the top of the world list: k_paths compacts its traversals block-wide
+    int n_mesh = 0;
+    V.mesh_obj = -1;
+    for (int k = 0; k < F.n_world; ++k)
+      if (F.objs[k].kind == OBJ_MESH) {
+        ++n_mesh;
+        V.mesh_obj = k;
+      }
+    if (n_mesh != 1) V.mesh_obj = -1;
+  }
   V.tri_pos = (const float4*)tp;
   V.tri_shade = ts;
   V.media = md;
@@ -209,7 +219,11 @@ static void accum_key(const srr_params* p, int key[5]) {
   key[4] = whole ? 0 : p->tile;
 }
 
-static int begin_accum(srr_renderer* r, const srr_params* p, int64_t npix, hipStream_t st, std::string& err) {
+// zero_pending (optional): the caller zeroes the sums itself (its first
+// accumulation starts from 0) instead of a memset here
+static int begin_accum(srr_renderer* r, const srr_params* p, int64_t npix, hipStream_t st, std::string& err,
+                       bool* zero_pending = nullptr) {
+  if (zero_pending) *zero_pending = false;
   int key[5];
   accum_key(p, key);
   if (p->flags & SRR_FLAG_CONTINUE) {
@@ -229,7 +243,8 @@ static int begin_accum(srr_renderer* r, const srr_params* p, int64_t npix, hipSt
     std::copy(key, key + 5, r->acc_key);
     return 0;
   }
-  RCHK(hipMemsetAsync(r->acc, 0, 3 * npix * sizeof(float), st));
+  if (zero_pending) *zero_pending = true;
+  else RCHK(hipMemsetAsync(r->acc, 0, 3 * npix * sizeof(float), st));
   r->acc_npix = npix;
   r->acc_samples = 0;
   std::copy(key, key + 5, r->acc_key);
@@ -350,10 +365,23 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
     r->pw_sample_cap = win_paths;
   }
   if (!r->pw_ctr) RCHK(hipMalloc((void**)&r->pw_ctr, 16 * sizeof(unsigned long long)));
+  if (!r->pw_ctr_host) RCHK(hipHostMalloc((void**)&r->pw_ctr_host, 16 * sizeof(unsigned long long)));
   RCHK(hipMemsetAsync(r->pw_ctr, 0, 16 * sizeof(unsigned long long), st));
+  // the sums of a fresh frame are zeroed by the first window's accumulation (init)
+  bool zero_pending = false;
   {
-    const int rc = begin_accum(r, p, npix, st, err);
+    const int rc = begin_accum(r, p, npix, st, err, p->spp > 0 ? &zero_pending : nullptr);
     if (rc < 0) return rc;
+  }
+  const int64_t acc_total = r->acc_samples + p->spp;
+  const bool want_sums = (p->flags & SRR_FLAG_SUMS) != 0;
+  // per-window HIP events around k_paths, read once the frame is done (no host
+  // round trip between windows)
+  const int n_windows = (p->spp + W - 1) / W;
+  while ((int)r->win_ev.size() < 2 * n_windows) {
+    hipEvent_t e;
+    RCHK(hipEventCreate(&e));
+    r->win_ev.push_back(e);
   }
   AccCommit commit{r};
   const bool all_fam = !r->diffuse_only;
@@ -370,6 +398,10 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
   // wave (kernels.hip coop_mixture); SRR_DEEP_TRIES=0 forces that branch (tests)
   const char* dt_env = getenv("SRR_DEEP_TRIES");
   const int deep_tries = dt_env ? std::max(0, atoi(dt_env)) : 32;
+#ifdef SRR_SLOW_RAYS
+  if (!r->pw_slow) RCHK(hipMalloc((void**)&r->pw_slow, (16 * 65536 + 16) * sizeof(float)));
+  RCHK(hipMemsetAsync(r->pw_slow + 16 * 65536, 0, 16 * sizeof(float), st));
+#endif
   RCHK(hipEventRecord(r->ev_beg, st));
   double kernel_ms = 0;
   for (int s0 = 0; s0 < p->spp; s0 += W) {
@@ -401,16 +433,22 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
     w.gstack_cap = gst_cap;
     w.wave_times = wave_times;
     w.deep_tries = deep_tries;
-    RCHK(hipMemsetAsync(w.cursor, 0, sizeof(unsigned long long), st));
-    RCHK(hipEventRecord(r->lanes[0].ev_t0, st));
+    w.dbg = getenv("SRR_PATHS_DBG") ? atoi(getenv("SRR_PATHS_DBG")) : 0;
+    w.slow_rays = r->pw_slow;
+    w.slow_count = r->pw_slow ? (unsigned*)(r->pw_slow + 16 * 65536) : nullptr;
+    const int wi = s0 / W;
+    if (wi > 0) RCHK(hipMemsetAsync(w.cursor, 0, sizeof(unsigned long long), st));  // window 0: zeroed with pw_ctr
+    RCHK(hipEventRecord(r->win_ev[2 * wi], st));
     launch_paths(r->view, w, all_fam ? 1 : 0, st);
-    RCHK(hipEventRecord(r->lanes[0].ev_t1, st));
-    launch_accumulate_window(r->pw_sample, (int)npix, Wn, r->acc, st);
-    RCHK(hipEventSynchronize(r->lanes[0].ev_t1));
-    float ms = 0;
-    RCHK(hipEventElapsedTime(&ms, r->lanes[0].ev_t0, r->lanes[0].ev_t1));
-    kernel_ms += ms;
+    RCHK(hipEventRecord(r->win_ev[2 * wi + 1], st));
+    // the last window also writes the output (k_finish fused): means, or raw sums (SRR_FLAG_SUMS)
+    const bool last = s0 + Wn >= p->spp;
+    launch_accumulate_window(r->pw_sample, (int)npix, Wn, r->acc, st, wi == 0 && zero_pending, last ? d_mean : nullptr,
+                             want_sums ? 0 : (int)acc_total);
     if (wave_times) {  // realtime clock: 100 MHz (10 ns ticks)
+      RCHK(hipEventSynchronize(r->win_ev[2 * wi + 1]));
+      float ms = 0;
+      RCHK(hipEventElapsedTime(&ms, r->win_ev[2 * wi], r->win_ev[2 * wi + 1]));
       std::vector<unsigned long long> wt(4 * (size_t)n_waves);
       RCHK(hipMemcpy(wt.data(), wave_times, wt.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
       std::vector<std::pair<double, int>> ex;
@@ -438,22 +476,46 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
     }
     s.trace_launches += 1;
   }
-  const int64_t acc_total = r->acc_samples + p->spp;
-  if (p->flags & SRR_FLAG_SUMS)
-    RCHK(hipMemcpyAsync(d_mean, r->acc, 3 * (size_t)npix * sizeof(float), hipMemcpyDeviceToDevice, st));
-  else
-    launch_finish(r->acc, d_mean, npix, (int)acc_total, st);
+  if (n_windows == 0) {  // spp 0: nothing rendered, the output is the sums as they stand
+    if (want_sums)
+      RCHK(hipMemcpyAsync(d_mean, r->acc, 3 * (size_t)npix * sizeof(float), hipMemcpyDeviceToDevice, st));
+    else
+      launch_finish(r->acc, d_mean, npix, (int)acc_total, st);
+  }
+  RCHK(hipMemcpyAsync(r->pw_ctr_host, r->pw_ctr, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
   RCHK(hipEventRecord(r->ev_end, st));
   RCHK(hipStreamSynchronize(st));
   RCHK(hipGetLastError());
-  unsigned long long ctr[16] = {0};
-  RCHK(hipMemcpy(ctr, r->pw_ctr, sizeof(ctr), hipMemcpyDeviceToHost));
+  for (int wi = 0; wi < n_windows; ++wi) {
+    float ms = 0;
+    RCHK(hipEventElapsedTime(&ms, r->win_ev[2 * wi], r->win_ev[2 * wi + 1]));
+    kernel_ms += ms;
+  }
+  unsigned long long ctr[16];
+  std::memcpy(ctr, r->pw_ctr_host, sizeof(ctr));
   if (getenv("SRR_PATHS_TIMING") && ctr[9]) {
     const double it = (double)ctr[9];
     fprintf(stderr, "k_paths per wave-iteration (ticks): refill %.0f  world %.0f  mesh %.0f  record %.0f  scatter %.0f  fold %.0f  (%llu wave-iterations)\n",
             ctr[4] / it, ctr[5] / it, ctr[6] / it, ctr[10] / it, (ctr[7] - ctr[10]) / it, ctr[8] / it, ctr[9]);
     fprintf(stderr, "  scatter: mixture loop %.0f ticks, %.2f rounds per wave-iteration\n", ctr[13] / it, ctr[14] / it);
   }
+#ifdef SRR_SLOW_RAYS
+  {  // diagnostics build: dump the slow world hits' records (one line per lane, JSON)
+    unsigned n = 0;
+    RCHK(hipMemcpy(&n, r->pw_slow + 16 * 65536, sizeof(unsigned), hipMemcpyDeviceToHost));
+    n = std::min(n, 65536u);
+    std::vector<float> v(16 * (size_t)n);
+    if (n) RCHK(hipMemcpy(v.data(), r->pw_slow, v.size() * sizeof(float), hipMemcpyDeviceToHost));
+    auto I = [&](size_t k) { int x; memcpy(&x, &v[k], 4); return x; };
+    for (unsigned i = 0; i < n; ++i) {
+      const size_t b = 16 * (size_t)i;
+      fprintf(stderr, "SLOWRAY {\"g\": %d, \"depth\": %d, \"o\": [%.9g, %.9g, %.9g], \"d\": [%.9g, %.9g, %.9g], "
+              "\"tm\": %.9g, \"ticks\": %d, \"steps\": %d, \"obj\": %d, \"prim\": %d, \"t\": %.9g, \"slot\": %d, "
+              "\"t0\": %d, \"spp_w\": %d}\n", I(b), I(b + 1), v[b + 2], v[b + 3], v[b + 4], v[b + 5], v[b + 6], v[b + 7], v[b + 8],
+              I(b + 9), I(b + 10), I(b + 11), I(b + 12), v[b + 13], I(b + 14), I(b + 15), p->spp);
+    }
+  }
+#endif
   const unsigned long long rays = ctr[0];
   if (ctr[2]) {
     err = "k_paths index guard tripped (bits " + std::to_string(ctr[2]) + ")";
@@ -733,7 +795,10 @@ srr_renderer::~srr_renderer() {
   (void)hipFree(pw_raw);
   (void)hipFree(pw_rays);
   (void)hipFree(pw_ctr);
+  if (pw_ctr_host) (void)hipHostFree(pw_ctr_host);
+  for (hipEvent_t e : win_ev) (void)hipEventDestroy(e);
   (void)hipFree(pw_wave_times);
+  (void)hipFree(pw_slow);
   for (auto& L : lanes) {
     srr::free_lane_paths(L);
     (void)hipFree(L.cnt);

@@ -77,6 +77,9 @@ struct srr_renderer {
   size_t pw_sample_cap = 0;
   unsigned long long* pw_ctr = nullptr;  // [0] world rays, [1] path cursor
   unsigned long long* pw_wave_times = nullptr;  // SRR_WAVE_TIMES diagnostics, 4 words per wave
+  unsigned long long* pw_ctr_host = nullptr;    // pinned mirror of pw_ctr, read after the frame's stream sync
+  std::vector<hipEvent_t> win_ev;               // per sample window: k_paths start / end
+  float* pw_slow = nullptr;  // diagnostics build (-DSRR_SLOW_RAYS): slow world-hit records + count
   int32_t* pixels = nullptr;
   size_t pix_cap = 0;
   // the shard whose pixel list (srr_shard_pixels) the renderer holds: {nx, ny,
