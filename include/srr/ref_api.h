@@ -134,6 +134,15 @@ class noise_texture : public texture {  // texture.h:35-46
  public:
   noise_texture(float sc) { handle = check(srr_noise_texture(cur(), sc)); }
 };
+/* srr extension (not a reference class): an image_texture over a synthetic RGB8
+ * image (srr_image_texture_gen; kind 0 sky, 1 wood, 2 checker) -- the BASELINE
+ * stand-in scenes' textures, generated in code instead of read from contents/. */
+class generated_texture : public texture {
+ public:
+  generated_texture(int nx, int ny, unsigned seed, int kind) {
+    handle = check(srr_image_texture_gen(cur(), nx, ny, seed, kind));
+  }
+};
 
 /* ----------------------------------------------------------------- materials */
 class material {  // material.h:82-93

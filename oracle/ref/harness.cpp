@@ -347,6 +347,53 @@ int cmd_sums(int argc, char** argv) {
   return 0;
 }
 
+// paths <scene.txt> <nx> <ny> <ns> <maxdepth> <pixels, comma-separated PPM-order indices> <out_prefix>:
+// every path of the listed pixels of the nx x ny frame (out.paths.f32 [n][ns][3]
+// raw color(), out.rays.u8 [n][ns] world rays) -- goldens for chosen pixels of a
+// frame too large to keep whole (tests/golden/make_tail.py)
+int cmd_paths(int argc, char** argv) {
+  if (argc < 9) return 2;
+  RefScene S = build(srr_text::parse(srr_text::read_file(argv[2])));
+  nx = atoi(argv[3]);
+  ny = atoi(argv[4]);
+  ns = atoi(argv[5]);
+  maxDepth = atoi(argv[6]);
+  std::vector<int> pixels;
+  for (const char* q = argv[7]; *q;) {
+    pixels.push_back(atoi(q));
+    while (*q && *q != ',') ++q;
+    if (*q == ',') ++q;
+  }
+  const std::string out = argv[8];
+  counting_world cw(S.world);
+  double** sp = sobol(ns);
+  std::vector<float> paths(pixels.size() * ns * 3);
+  std::vector<unsigned char> rays(pixels.size() * ns);
+  for (size_t q = 0; q < pixels.size(); ++q) {
+    const int pix = pixels[q];
+    int i = pix % nx;
+    int j = ny - 1 - pix / nx;
+    for (int s = 0; s < ns; ++s) {
+      reseed_path((unsigned)i, (unsigned)j, (unsigned)s);
+      float u = float(sp[s][0] + i) / float(nx);
+      float v = float(sp[s][1] + j) / float(ny);
+      ray r = S.cam->get_ray(u, v);
+      int depth = 0;
+      long long before = cw.n;
+      vec3 c = color(r, &cw, S.lights, &depth);
+      const size_t k = q * ns + s;
+      paths[3 * k] = c[0];
+      paths[3 * k + 1] = c[1];
+      paths[3 * k + 2] = c[2];
+      rays[k] = (unsigned char)(cw.n - before);
+    }
+  }
+  write(out + ".paths.f32", paths.data(), paths.size() * 4);
+  write(out + ".rays.u8", rays.data(), rays.size());
+  printf("{\"pixels\": %zu, \"world_rays\": %lld}\n", pixels.size(), cw.n);
+  return 0;
+}
+
 int cmd_render(int argc, char** argv) {
   if (argc < 8) return 2;
   RefScene S = build(srr_text::parse(srr_text::read_file(argv[2])));
@@ -511,6 +558,7 @@ int main(int argc, char** argv) {
     std::string c = argv[1];
     if (c == "render") return cmd_render(argc, argv);
     if (c == "sums") return cmd_sums(argc, argv);
+    if (c == "paths") return cmd_paths(argc, argv);
     if (c == "bvh") return cmd_bvh(argc, argv);
     if (c == "teapot") return cmd_teapot(argc, argv);
     if (c == "sobol") return cmd_sobol(argc, argv);

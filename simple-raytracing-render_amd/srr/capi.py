@@ -210,6 +210,21 @@ def tonemap(mean: np.ndarray) -> np.ndarray:
     return out
 
 
+def scene_digest(text: str) -> str:
+    """srr_scene_digest of a scene description: the FNV-1a digest of its
+    flattened device tables (hex), equal for byte-identical scenes."""
+    L = lib()
+    L.srr_scene_digest.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p]
+    h = ctypes.c_void_p()
+    _check(L.srr_scene_from_text(text.encode(), ctypes.byref(h)))
+    d = ctypes.c_uint64()
+    try:
+        _check(L.srr_scene_digest(h, ctypes.byref(d), None))
+    finally:
+        L.srr_scene_destroy(h)
+    return f"{d.value:016x}"
+
+
 def write_ppm(path: str, nx: int, ny: int, img8: np.ndarray) -> None:
     img8 = np.ascontiguousarray(img8, np.uint8)
     _check(lib().srr_write_ppm(path.encode(), nx, ny, _ptr(img8)))

@@ -315,3 +315,28 @@ def flatnormal_bunny(aspect: float, contents: str | None = None) -> Scene:
 BY_SCENEID = {0: cornell_box, 1: teapot_scene, 2: ball_scenes, 3: ball_orennayar_scenes, 4: jadebunny_scene,
               5: final, 6: soldier_scene, 7: flatnormal_bunny}
 BUILDERS = {f.__name__: f for f in list(BY_SCENEID.values()) + [random_scene]}
+
+
+def main(argv=None) -> int:
+    """Write one of the reference's scenes as an srr scene description, for
+    programs that take one (render_main --scene-text, srr_scene_from_text):
+
+        python -m srr.ref_scenes --sceneid 2 [--aspect 1.0] [--contents DIR] > balls.scene
+    """
+    import argparse
+    import sys
+    ap = argparse.ArgumentParser(prog="python -m srr.ref_scenes")
+    ap.add_argument("--sceneid", type=int, choices=sorted(BY_SCENEID))
+    ap.add_argument("--builder", choices=sorted(BUILDERS))
+    ap.add_argument("--aspect", type=float, default=1.0)
+    ap.add_argument("--contents", default=None)
+    a = ap.parse_args(argv)
+    if (a.sceneid is None) == (a.builder is None):
+        ap.error("give one of --sceneid / --builder")
+    f = BY_SCENEID[a.sceneid] if a.builder is None else BUILDERS[a.builder]
+    sys.stdout.write(f(a.aspect, contents=a.contents).text())
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -7,13 +7,17 @@ per-path radiance bits (NaN payloads aside) and the mean image.
 
 On a mismatch, with SRR_DIAG_DIR set, the failing pixels' per-path outputs are
 saved there for bisection against the CPU restatement (tools/diag_fullframe.py)."""
+import json
 import os
 
 import numpy as np
 import pytest
 
 import fullframe
+import parity
 from srr import capi
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 pytestmark = pytest.mark.gpu
 
@@ -52,3 +56,12 @@ def test_c2_full_frame_is_the_reference_frame(mode, monkeypatch):
     assert out["stats"]["world_rays"] == m["world_rays"], res
     assert res["ray_mismatch_pixels"] == 0 and res["hash_mismatch_pixels"] == 0, res
     assert res["mean_mismatch_pixels"] == 0, res
+    # the tail pixels (NaN-bound world hits, tests/golden/make_tail.py): every
+    # path's radiance bits and world rays against the reference's own paths
+    tail = json.load(open(os.path.join(GOLDEN, "c2_tail.json")))
+    tp = np.array(tail["pixels"])
+    gp = np.fromfile(os.path.join(GOLDEN, "c2_tail.paths.f32"), np.float32).reshape(len(tp), tail["spp"], 3)
+    gr = np.fromfile(os.path.join(GOLDEN, "c2_tail.rays.u8"), np.uint8).reshape(len(tp), tail["spp"])
+    pc = parity.compare_paths(out["paths"][tp], gp)
+    assert pc["bitexact"] == 1.0, pc
+    assert (out["rays"][tp] == gr).all()

@@ -10,6 +10,7 @@ import numpy as np
 import pytest
 
 import oracle_bind as ob
+import parity
 
 META = json.load(open(os.path.join(ob.GOLDEN, "golden.json")))
 
@@ -57,3 +58,20 @@ def test_render_threads_deterministic():
     a = ob.render(text, 16, 16, 4, 50, threads=1)
     b = ob.render(text, 16, 16, 4, 50, threads=4)
     np.testing.assert_array_equal(a["paths"].view(np.uint32), b["paths"].view(np.uint32))
+
+
+def test_restatement_matches_reference_tail_pixels():
+    """The C2 frame's NaN-bound pixels (tests/golden/make_tail.py: a ray in the
+    light's plane makes closest_so_far NaN before the teapot is tested): the
+    restatement's paths are the reference's, bit for bit."""
+    meta = json.load(open(os.path.join(ob.GOLDEN, "c2_tail.json")))
+    text = open(os.path.join(ob.GOLDEN, meta["scene"])).read()
+    pix = np.array(meta["pixels"], np.int32)
+    n, spp = len(pix), meta["spp"]
+    gp = np.fromfile(os.path.join(ob.GOLDEN, "c2_tail.paths.f32"), np.float32).reshape(n, spp, 3)
+    gr = np.fromfile(os.path.join(ob.GOLDEN, "c2_tail.rays.u8"), np.uint8).reshape(n, spp)
+    r = ob.render(text, meta["nx"], meta["ny"], spp, meta["max_depth"], pixels=pix, threads=8)
+    pc = parity.compare_paths(r["paths"], gp)
+    assert pc["bitexact"] == 1.0, pc
+    assert (r["rays"] == gr).all()
+    assert int(r["stats"][0]) == meta["world_rays"]
