@@ -35,7 +35,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--scene", default="s2", choices=["s1", "s2", "s3", "s3_metal", "s4", "s5"])
+    ap.add_argument("--scene", default="s2", choices=["s1", "s2", "s3", "s3_metal", "s4", "s5", "s4_real"],
+                    help="s4_real: the reference's real soldier_scene (Soilder.FBX, sky4.jpg; Raytracing_n.cpp:585-657) "
+                         "from its committed fixture (tests/golden/make_soldier.py), 1920x1080x1024")
     ap.add_argument("--divs", type=int, default=0,
                     help="teapot subdivision (s2/s3: 10 = 6,400 tris; 100 = the reference's as-shipped 640,000, "
                          "teapot.h:77; s4/s5: 40 = 102,400)")
@@ -61,7 +63,20 @@ def parse():
     return ap.parse_args()
 
 
-CONFIG_KEY = {"s1": "C1", "s2": "C2", "s3": "C3", "s3_metal": "C3_metal", "s4": "C4", "s5": "C5"}
+CONFIG_KEY = {"s1": "C1", "s2": "C2", "s3": "C3", "s3_metal": "C3_metal", "s4": "C4", "s5": "C5", "s4_real": "C4_real"}
+
+
+class _TextScene:
+    def __init__(self, text):
+        self._t = text
+
+    def text(self):
+        return self._t
+
+
+def _soldier_real():
+    import soldier_fixture
+    return _TextScene(soldier_fixture.scene_text()), dict(nx=1920, ny=1080, spp=1024, max_depth=50)
 
 
 def cpu_baseline(text, nx, ny, spp, budget_s):
@@ -162,12 +177,13 @@ def main():
     host_reduce = world > 1 and backend == "gloo"
 
     dv = {"divs": a.divs} if a.divs else {}
-    if a.divs and a.scene == "s1":
-        raise SystemExit("--divs: s1 has no teapot")
+    if a.divs and a.scene in ("s1", "s4_real"):
+        raise SystemExit(f"--divs: {a.scene} has no teapot")
     fac = {"s1": scenes.s1_cornell, "s2": lambda: scenes.s2_cornell_teapot(**dv),
            "s3": lambda: scenes.s3_cornell_teapot_microfacet(**dv),
            "s3_metal": lambda: scenes.s3_cornell_teapot_microfacet("metal", **dv),
-           "s4": lambda: scenes.s4_soldier_standin(**dv), "s5": lambda: scenes.s5_soldier_fog(**dv)}[a.scene]
+           "s4": lambda: scenes.s4_soldier_standin(**dv), "s5": lambda: scenes.s5_soldier_fog(**dv),
+           "s4_real": _soldier_real}[a.scene]
     sc, cfg = fac()
     nx, ny, spp = a.nx or cfg["nx"], a.ny or cfg["ny"], a.spp or cfg["spp"]
     text = sc.text()
@@ -253,7 +269,9 @@ def main():
             "scaling": "weak" if a.plan == "samples" else "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (scene built in code: Cornell box + tessellated Utah teapot)",
+            "data": ("the reference's own assets (Soilder.FBX mesh 0, sky4.jpg, textures) via the committed fixture"
+                     if a.scene == "s4_real" else
+                     "synthetic (scene built in code: Cornell box + tessellated Utah teapot)"),
             "config": {"workload": f"{key}: {a.scene}{f' divs {a.divs}' if a.divs else ''} {nx}x{ny} {spp}spp "
                                    f"maxDepth {cfg['max_depth']}" + (
                                    (f", {a.tile}x{a.tile} tiles round-robin over {world} GPUs, one {coll} gather "
@@ -276,6 +294,28 @@ def main():
                          "measured_bound": "issue/latency: the scene lives in LDS and L2, measured HBM traffic is a "
                                            "few % of peak (profiles/r02/counters_*.json)"},
         }
+        # issue roofline of the same kernel from a committed PMC summary of this build
+        # (tools/counters.sh -> profiles/r03/counters_<scene>.json): VALU wave-instructions
+        # per launch over the live launch time, against 1,024 SIMDs each issuing one
+        # wave64 VALU instruction per 2 cycles (SIMD-32, MI355X_MICROARCH.md)
+        cnt = os.path.join(ROOT, "profiles", "r03", f"counters_{a.scene}{key[len(CONFIG_KEY[a.scene]):]}.json")
+        if os.path.exists(cnt) and trace_ms > 0:
+            cj = json.load(open(cnt))
+            insts = cj["raw_per_launch"]["SQ_INSTS_VALU"]
+            clock = cj.get("clock_ghz") or 2.4
+            rate = insts / (trace_ms / max(launches, 1) * 1e-3)
+            peak = 1024 * clock * 1e9 / 2
+            lane = cj.get("valu_lane_utilisation")
+            out["roofline"]["issue"] = {
+                "valu_wave_insts_per_s": round(rate, -6), "peak": round(peak, -6), "frac": round(rate / peak, 4),
+                "lane_utilisation": lane, "lane_frac": round(rate / peak * lane, 4) if lane else None,
+                "wave_time_split": cj.get("wave_time_split"), "clock_ghz": clock,
+                "source": os.path.relpath(cnt, ROOT) + f" ({cj.get('ms_per_launch_profiled')} ms/launch profiled)"}
+            ws = cj.get("wave_time_split") or {}
+            out["roofline"]["measured_bound"] = (
+                f"latency/issue: VALU pipe {100 * rate / peak:.0f}% busy at {100 * (lane or 0):.0f}% lane "
+                f"utilisation, waves {100 * ws.get('waiting_on_memory_or_barrier', 0):.0f}% of their time waiting; "
+                f"HBM {100 * (out['roofline']['traffic_GBps'] or 0) / HBM_PEAK_GBS:.1f}% of peak")
         if a.count_visits:
             out["visits"] = {"box_tests_per_ray": visits[0] / max(rays, 1), "tri_tests_per_ray": visits[1] / max(rays, 1),
                              "stack_overflows": visits[2], "note": "counting run: timing not representative"}

@@ -19,6 +19,7 @@ sys.path.insert(0, os.path.join(ROOT, "simple-raytracing-render_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 import oracle_bind as ob  # noqa: E402
+import soldier_fixture  # noqa: E402
 from srr import scenes  # noqa: E402
 
 CONFIGS = {
@@ -30,7 +31,17 @@ CONFIGS = {
     "C5": (scenes.s5_soldier_fog, 192, 108, 8),
     # C2 with the reference's as-shipped teapot (teapot.h:77: divs 100, 640,000 triangles)
     "C2_d100": (lambda: scenes.s2_cornell_teapot(divs=100), 96, 96, 16),
+    # the reference's real soldier_scene (Raytracing_n.cpp:585-657) from its fixture
+    "C4_real": (lambda: (_Text(soldier_fixture.scene_text()), None), 192, 108, 8),
 }
+
+
+class _Text:
+    def __init__(self, t):
+        self.t = t
+
+    def text(self):
+        return self.t
 
 
 def main():
@@ -38,7 +49,7 @@ def main():
     for name, (fac, nx, ny, spp) in CONFIGS.items():
         sc, _ = fac()
         r = ob.render(sc.text(), nx, ny, spp, 50, threads=os.cpu_count() or 4, want_paths=False)
-        w, node, tri, prim = (int(x) for x in r["stats"])
+        w, node, tri, prim = (int(x) for x in r["stats"][:4])
         paths = nx * ny * spp
         n_node, n_tri, n_prim = node / w, tri / w, prim / w
         out[name] = dict(sample=f"{nx}x{ny}x{spp}", paths=paths, world_rays=w, rays_per_path=w / paths,

@@ -97,7 +97,7 @@ def test_reference_builders_through_render_main(tmp_path):
 
 @pytest.mark.gpu
 def test_render_main_image_is_the_python_render(exe, tmp_path):
-    nx, ny, ns = 48, 32, 4
+    nx, ny, ns = 40, 40, 4  # square: scenes.s2_cornell_teapot's camera has aspect 1
     out = str(tmp_path / "o.ppm")
     r = subprocess.run([exe, "--scene", "s2", "--nx", str(nx), "--ny", str(ny), "--ns", str(ns), "--out", out],
                        capture_output=True, text=True, timeout=300)

@@ -1,0 +1,52 @@
+"""The reference's real C4 scene, soldier_scene (Raytracing_n.cpp:585-657: the
+Soilder.FBX mesh 0 scaled 8 and turned 180 degrees, textured Beckmann, the
+wooden Oren-Nayar floor box in a glass slab, the sky4.jpg environment sphere,
+aperture 10), rendered from its committed fixture (tests/golden/make_soldier.py).
+The assets go through srr's own loaders; their parity against assimp is unpinned
+(its binaries are Win32 only), against stb_image it is byte-exact
+(tests/test_imageio.py).  GPU: 1920x1080 sampled pixels against the CPU
+restatement, bit-exact."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_bind as ob
+import parity
+import soldier_fixture
+from srr import capi, ref_scenes
+
+CONTENTS = "/root/reference/contents"
+
+
+def test_fixture_restores_the_scene():
+    text = soldier_fixture.scene_text()
+    assert text.count(" triangle_uvn ") == 3971  # Soilder.FBX mesh 0 after triangulation
+    if os.path.isdir(CONTENTS):  # the development container: rebuilt from the reference's assets
+        want = ref_scenes.soldier_scene(1920 / 1080, contents=CONTENTS).text()
+        assert capi.scene_digest(text) == capi.scene_digest(want)
+    else:
+        assert len(capi.scene_digest(text)) == 16
+
+
+def test_restatement_renders_fixture_pixels():
+    r = ob.render(soldier_fixture.scene_text(), 1920, 1080, 2, 50, pixels=np.arange(960 * 1080 + 600, 960 * 1080 + 632,
+                                                                                     dtype=np.int32), threads=4)
+    assert int(r["stats"][0]) > 0 and np.isfinite(r["img"]).all()
+
+
+@pytest.mark.gpu
+def test_gpu_soldier_scene_sampled_pixels_match_restatement():
+    text = soldier_fixture.scene_text()
+    nx, ny, spp = 1920, 1080, 4
+    out = capi.Renderer(text).render(nx, ny, spp, 50, keep_paths=True)
+    rng = np.random.default_rng(11)
+    # 300 pixels over the frame and 200 in the window around the soldier
+    x0, x1, y0, y1 = 700, 1220, 250, 1000
+    win = (rng.integers(y0, y1, 200) * nx + rng.integers(x0, x1, 200))
+    pix = np.unique(np.concatenate([rng.choice(nx * ny, 300, replace=False), win])).astype(np.int32)
+    ref = ob.render(text, nx, ny, spp, 50, pixels=pix, threads=min(16, os.cpu_count() or 4))
+    pc = parity.compare_paths(out["paths"][pix], ref["paths"])
+    print(pc, "world rays", out["stats"]["world_rays"])
+    assert pc["bitexact"] >= parity.MIN_BITEXACT, pc
+    assert (out["rays"][pix] == ref["rays"]).all()
