@@ -74,6 +74,14 @@ struct TriShade {  // triangle.h fields used after a hit
   int32_t mat;
 };
 
+// Compressed 4-wide node (Flat::node4q), 16 words = 64 B, same index and child
+// references as the 128-B node: origin xyz, scale xyz (powers of two), then per
+// bound one word of 4 bytes (child c in byte c): lo.x lo.y lo.z hi.x hi.y hi.z,
+// then the 4 child references.  Child c's box on axis a is
+//   [o_a + q_lo * s_a, o_a + q_hi * s_a]   (float mul, then float add)
+// which contains the child's exact box (the builder checks the rounding).
+constexpr int kNode4qWords = 16;
+
 struct DMesh {
   int32_t node_off;  // into node arrays (root = node_off)
   int32_t tri_off;   // into tri arrays

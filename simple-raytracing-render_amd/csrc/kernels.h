@@ -21,6 +21,9 @@ struct SceneView {  // device pointers into the flattened tables (device_scene.h
   const float4* nodes;  // 2 float4 per BVH2 node: lo (min.xyz, skip), hi (max.xyz, leaf)
   const float4* node4;  // 8 float4 per 4-wide node (device_scene.h), breadth-first per mesh
   int node4_lds;        // leading nodes the path kernel keeps in LDS (<= kPathsLdsNodes)
+  const float4* node4q; // the same nodes compressed to 64 B (device_scene.h kNode4qWords), or nullptr
+  int node4_lds_q;      // ...and how many of those the path kernel keeps in LDS (<= 2 kPathsLdsNodes)
+  int use_q;            // k_paths traces meshes over node4q (SRR_CBVH)
   int quad_trace;       // k_paths traces meshes quad-cooperatively (BVH4 larger than an XCD's L2)
   int quad_max;         // ...when at most this many lanes of the wave enter the mesh (else per lane)
   int mesh_obj;         // the world list's one top-level mesh object (k_paths CMP variant), else -1

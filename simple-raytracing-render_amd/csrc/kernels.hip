@@ -321,9 +321,28 @@ SRR_D void mesh_scan_nan(const SceneView& S, const DMesh& m, const Ray& r, bool 
   }
 }
 
+// one axis of a slab test on the whole line (as SRR_CHILD's): entry / exit
+SRR_D void slab_axis(float L, float H, float O, float I, float& lo, float& hi) {
+  const float t0 = (L - O) * I, t1 = (H - O) * I;
+  const bool sw = I < 0.0f;
+  const float n = sw ? t1 : t0, f = sw ? t0 : t1;
+  lo = n > lo ? n : lo;
+  hi = f < hi ? f : hi;
+}
+
+// A compressed node's box bound (device_scene.h kNode4qWords): o + q * s with
+// q = byte c of the word, one float multiply (exact) and one float add
+SRR_D float q_bound(float o, float s, uint32_t w, int c) { return o + (float)((w >> (8 * c)) & 255u) * s; }
+
 // 4-wide traversal of one mesh; same result as mesh_hit (the reference's
 // leaf set, min t, ties to the later DFS triangle).
-template <bool PRUNE, bool TIMING = false>
+// Q: the 64-B compressed nodes (SceneView::node4q): inner children are tested
+// against their outward-rounded boxes (a larger box only visits and prunes
+// less), leaf children against the rounded box first and then against their
+// exact box, recomputed from the leaf's 1-2 triangles (ffmin / ffmax of the
+// vertices: the reference's triangle / bvh_node box, triangle.h:53-68) with the
+// reference's slab arithmetic -- the same leaf set as the 128-B nodes.
+template <bool PRUNE, bool TIMING = false, bool Q = false>
 SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmin, float tmax, bool is_medium,
                      MeshHit& out, const TraceCtx& cx) {
   if (const uint64_t nanm = __ballot(!(tmax == tmax))) {  // NaN bound: the fold over all triangles
@@ -356,7 +375,24 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
   for (;;) {
     float4 LX, LY, LZ, HX, HY, HZ;
     int4 CH;
-    if (node < cx.lds_count) {  // top levels: LDS copy (k_paths)
+    if constexpr (Q) {
+      f32x4 A, B, C, D;
+      if (node < cx.lds_count) {  // top levels: LDS copy (k_paths)
+        const __attribute__((address_space(3))) f32x4* N = cx.lds_nodes + 4 * node;
+        A = N[0], B = N[1], C = N[2], D = N[3];
+      } else {
+        const f32x4* N = (const f32x4*)(S.node4q + 4 * (size_t)node);
+        A = N[0], B = N[1], C = N[2], D = N[3];
+      }
+      // A = (o.x, o.y, o.z, s.x), B = (s.y, s.z, lo.x, lo.y), C = (lo.z, hi.x, hi.y, hi.z), D = children
+      const uint32_t qlx = __float_as_uint(B[2]), qly = __float_as_uint(B[3]), qlz = __float_as_uint(C[0]);
+      const uint32_t qhx = __float_as_uint(C[1]), qhy = __float_as_uint(C[2]), qhz = __float_as_uint(C[3]);
+#define SRR_QB(O, S_, W) make_float4(q_bound(O, S_, W, 0), q_bound(O, S_, W, 1), q_bound(O, S_, W, 2), q_bound(O, S_, W, 3))
+      LX = SRR_QB(A[0], A[3], qlx), LY = SRR_QB(A[1], B[0], qly), LZ = SRR_QB(A[2], B[1], qlz);
+      HX = SRR_QB(A[0], A[3], qhx), HY = SRR_QB(A[1], B[0], qhy), HZ = SRR_QB(A[2], B[1], qhz);
+#undef SRR_QB
+      CH = make_int4(__float_as_int(D[0]), __float_as_int(D[1]), __float_as_int(D[2]), __float_as_int(D[3]));
+    } else if (node < cx.lds_count) {  // top levels: LDS copy (k_paths)
       const __attribute__((address_space(3))) f32x4* N = cx.lds_nodes + 8 * node;
       auto f4 = [](f32x4 v) { return make_float4(v[0], v[1], v[2], v[3]); };
       LX = f4(N[0]), LY = f4(N[1]), LZ = f4(N[2]), HX = f4(N[3]), HY = f4(N[4]), HZ = f4(N[5]);
@@ -398,10 +434,27 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
       if (!hit[c] || ch[c] >= 0 || ch[c] == INT32_MIN) continue;
       const int leaf = ~ch[c];
       const int first = leaf >> 1, count = (leaf & 1) + 1;
+      if constexpr (Q) {  // the exact leaf box from the vertices (the tests below re-read them from L1)
+        const float4* tp = S.tri_pos + kTriStride * (size_t)first;
+        V3 mn, mx;
+        for (int t = 0; t < count; ++t) {
+          const float4 a = tp[kTriStride * t], b = tp[kTriStride * t + 1], cc = tp[kTriStride * t + 2];
+          const V3 tmn = v3(ffmin(ffmin(a.x, b.x), cc.x), ffmin(ffmin(a.y, b.y), cc.y), ffmin(ffmin(a.z, b.z), cc.z));
+          const V3 tmx = v3(ffmax(ffmax(a.x, b.x), cc.x), ffmax(ffmax(a.y, b.y), cc.y), ffmax(ffmax(a.z, b.z), cc.z));
+          mn = t ? v3(ffmin(mn.x, tmn.x), ffmin(mn.y, tmn.y), ffmin(mn.z, tmn.z)) : tmn;
+          mx = t ? v3(ffmax(mx.x, tmx.x), ffmax(mx.y, tmx.y), ffmax(mx.z, tmx.z)) : tmx;
+        }
+        float lo_ = -INFINITY, hi_ = INFINITY;
+        slab_axis(mn.x, mx.x, r.o.x, inv.x, lo_, hi_);
+        slab_axis(mn.y, mx.y, r.o.y, inv.y, lo_, hi_);
+        slab_axis(mn.z, mx.z, r.o.z, inv.z, lo_, hi_);
+        const float a_ = lo_ > tmin ? lo_ : tmin, b_ = hi_ < tmax ? hi_ : tmax;
+        if ((b_ <= a_) || (PRUNE && lo_ > bound)) continue;  // the exact leaf box misses
+      }
       ntri += 2;
       for (int ti = first; ti < first + count; ++ti) {
         const float4* tp = S.tri_pos + kTriStride * (size_t)ti;
-        float4 a = tp[0], b = tp[1], cc = tp[2];
+        const float4 a = tp[0], b = tp[1], cc = tp[2];
         V3 p0 = v3(a.x, a.y, a.z), p1 = v3(b.x, b.y, b.z), p2 = v3(cc.x, cc.y, cc.z);
         float t, u, v;
         bool h = tri_hit(p0, p1, p2, true, r.o, dir, t, u, v);
@@ -515,6 +568,7 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
 // global extension).  Same visit rules, pruning and result as mesh_hit4; a quad
 // whose stack overflows leaves its ray to the exact BVH2 re-walk.
 constexpr int TR_QUAD = 32;
+constexpr int TR_Q = 64;  // meshes traced over the compressed 64-B nodes (SceneView::node4q)
 
 template <int CTRL>
 SRR_D int quad_dpp(int x) { return __builtin_amdgcn_update_dpp(x, x, CTRL, 0xF, 0xF, false); }
@@ -864,11 +918,15 @@ SRR_D bool basic_hit(const SceneView& S, const DObj& ob, const Ray& lr, float tm
                      ObjHit& h, const TraceCtx& cx) {
   switch (ob.kind) {
     case OBJ_MESH: {
+#ifdef SRR_EXP_NOMESH  // timing experiment only (wrong image): meshes never hit
+      return false;
+#endif
       MeshHit mh;
       const DMesh m = wload<TR>(S.meshes, ob.idx);
       bool hit;
       if (tr_mode(TR) == TR_BVH2) hit = mesh_hit<false>(S, m, lr, tmin, tmax, is_medium, mh, cx.ctr);
       else if (TR & TR_QUAD) hit = mesh_hit4_quad<tr_mode(TR) != TR_BVH4>(S, m, lr, tmin, tmax, is_medium, mh, cx);
+      else if (TR & TR_Q) hit = mesh_hit4<tr_mode(TR) != TR_BVH4, false, true>(S, m, lr, tmin, tmax, is_medium, mh, cx);
       else hit = mesh_hit4<tr_mode(TR) != TR_BVH4, tr_mode(TR) == TR_BVH4_TIMED>(S, m, lr, tmin, tmax, is_medium, mh, cx);
       if (!hit) return false;
       h.t = mh.t;
@@ -1921,6 +1979,23 @@ SRR_D int skip_mixture(const SceneView& S, const DiffSetup& me, bool dead, bool&
   return rounds;
 }
 
+// Point i of the reference's Sobol set for D = 2 (Raytracing_n.cpp:721-812, the
+// Joe-Kuo generator with direction numbers "1" and "2 1 0 1"), computed instead
+// of loaded: the generator's Gray-code recurrence X_i = X_{i-1} ^ V[c(i-1)] gives
+// X_i = XOR of V[k] over the set bits k of gray(i) = i ^ (i >> 1); dimension 1 has
+// V[k] = 2^(31-k) (so X = bit-reversed gray(i)), dimension 2 (s = 1, a = 0)
+// V[0] = 2^31, V[k] = V[k-1] ^ (V[k-1] >> 1).  Both are exact in double after the
+// division by 2^32.  Equal to the uploaded set point for point (the full-frame
+// and golden parity tests use every point); it saves each path start a global load.
+SRR_D void sobol2_point(uint32_t i, double& sx, double& sy) {
+  const uint32_t g = i ^ (i >> 1);
+  uint32_t y = 0, v = 0x80000000u;
+  for (uint32_t t = g; t; t >>= 1, v ^= v >> 1)
+    if (t & 1) y ^= v;
+  sx = (double)__builtin_bitreverse32(g) / 4294967296.0;
+  sy = (double)y / 4294967296.0;
+}
+
 // The camera ray of sample s_global of pixel `pix` with its per-path RNG streams
 // (SURVEY §8(d) seeding; Raytracing_n.cpp:827-836; camera::get_ray, camera.h:51-59).
 SRR_D void camera_ray(const SceneView& S, int pix, int s_global, double sx, double sy, int nx, int ny,
@@ -2296,7 +2371,8 @@ constexpr unsigned long long kPoolChunk = 64;  // path indices a wave takes per 
 // result of every ray is mesh_hit4's, so paths stay bit-identical.
 constexpr int kPathsLdsNodesCmp = 56;  // LDS node cache of the CMP variant (room for the queue)
 
-template <bool MEDIA, bool ALLFAM, int MINB, bool TIMED = false, bool WL = true, bool QUAD = false, bool CMP = false>
+template <bool MEDIA, bool ALLFAM, int MINB, bool TIMED = false, bool WL = true, bool QUAD = false, bool CMP = false,
+          bool CQ = false>
 __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathWork W) {
   static_assert(!CMP || (!MEDIA && !TIMED && WL && !QUAD), "CMP: world list in LDS, no media, per-lane walks");
   // TIMED (diagnostics): per-wave cycles in refill / world hit (mesh part) / record+scatter / fold
@@ -2307,7 +2383,7 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
   // WL: world tables staged in LDS (they fit in kWorldLdsBytes); otherwise read
   // from global memory (large object lists, e.g. random_scene's ~490 spheres)
   // QUAD: meshes traced by mesh_hit4_quad (large BVHs, SceneView::quad_trace)
-  constexpr int TR = TR_BVH4_PRUNE | (WL ? TR_WL : 0) | (QUAD ? TR_QUAD : 0);
+  constexpr int TR = TR_BVH4_PRUNE | (WL ? TR_WL : 0) | (QUAD ? TR_QUAD : 0) | (CQ ? TR_Q : 0);
   if constexpr (WL) {
     __shared__ uint4 s_world[kWorldLdsBytes / 16];
     for (int i = threadIdx.x; i < S0.world_words; i += blockDim.x) s_world[i] = S0.world_blob[i];
@@ -2327,9 +2403,13 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
   __shared__ int s_node[kStack * kPathsBlock];
   __shared__ float s_t[kStack * kPathsBlock];
   constexpr int kNodesLds = CMP ? kPathsLdsNodesCmp : kPathsLdsNodes;
-  const int n_lds_nodes = min(S0.node4_lds, kNodesLds);
+  // (CQ: the same LDS bytes hold twice as many 64-B nodes)
+  const int n_lds_nodes = CQ ? min(S0.node4_lds_q, 2 * kNodesLds) : min(S0.node4_lds, kNodesLds);
   __shared__ float4 s_n4[kNodesLds * 8];
-  for (int i = threadIdx.x; i < n_lds_nodes * 8; i += blockDim.x) s_n4[i] = S0.node4[i];
+  if (CQ)
+    for (int i = threadIdx.x; i < n_lds_nodes * 4; i += blockDim.x) s_n4[i] = S0.node4q[i];
+  else
+    for (int i = threadIdx.x; i < n_lds_nodes * 8; i += blockDim.x) s_n4[i] = S0.node4[i];
   // CMP: the mesh-ray queue, SoA [8][kPathsBlock]: origin, direction, t bound
   // (in) / hit t (out), triangle (out); per-wave queue counts | active bit
   __shared__ float s_q[CMP ? 8 * kPathsBlock : 1];
@@ -2395,8 +2475,9 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
         const int pix = W.pixels ? W.pixels[lp] : lp;
         V3 o, d;
         float tm;
-        camera_ray(S, pix, W.s_base + s, W.sobol[2 * s], W.sobol[2 * s + 1], W.nx, W.ny, W.base_seed, o, d, tm,
-                   rng);
+        double sx, sy;
+        sobol2_point((uint32_t)(W.s_base + (int)s), sx, sy);  // = W.sobol[2 s], W.sobol[2 s + 1]
+        camera_ray(S, pix, W.s_base + s, sx, sy, W.nx, W.ny, W.base_seed, o, d, tm, rng);
         r = Ray{o, d, tm};
         depth = 0;
       }
@@ -2585,6 +2666,9 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
         rounds = skip_mixture(S, ds, d_dead, pend, d_tries, rng.lcg, d_dir, d_pdf);
       } else {
         if (SRR_MIXTURE_SKIP == 2) rounds = skip_mixture(S, ds, d_dead, pend, d_tries, rng.lcg, d_dir, d_pdf, 1);
+#ifdef SRR_EXP_MIX1  // timing experiment only (wrong image): one attempt per loop
+        if (pend) { pend = false; d_pdf = 1.f; }
+#endif
         if (__ballot(pend)) rounds += coop_mixture(S, ds, pend, d_tries, rng.lcg, d_dir, d_pdf, W.deep_tries);
       }
       if (TIMED) {
@@ -3239,9 +3323,11 @@ void launch_paths(const SceneView& S, const PathWork& W, int all_families, hipSt
     return e && atoi(e) != 0;
   }();
   const bool cmp = compact && S.mesh_obj >= 0 && !S.has_media && !S.quad_trace && !timed;
+  const bool cq = S.use_q && !S.quad_trace && !timed && !cmp;  // compressed nodes, per-lane walks
 #define SRR_LAUNCH_PATHS(M, A, B)                                                                      \
   if (timed) hipLaunchKernelGGL((dev::k_paths<M, A, 4, true>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W); \
   else if (!M && cmp && B == 4) hipLaunchKernelGGL((dev::k_paths<false, A, 4, false, true, false, true>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W); \
+  else if (cq && B == 4) hipLaunchKernelGGL((dev::k_paths<M, A, 4, false, true, false, false, true>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W); \
   else if (S.quad_trace && B == 4) hipLaunchKernelGGL((dev::k_paths<M, A, 4, false, true, true>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W); \
   else hipLaunchKernelGGL((dev::k_paths<M, A, B>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W)
 #ifdef SRR_OCC_VARIANTS  // occupancy A/B builds (SRR_PATHS_OCC): 2, 3, 5 and 6 blocks per CU

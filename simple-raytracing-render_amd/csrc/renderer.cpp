@@ -55,6 +55,8 @@ int renderer_create(const Scene& sc, int device, srr_renderer** out, std::string
   RCHK(upload(&me, F.meshes, K));
   RCHK(upload(&nodes, F.nodes, K));
   RCHK(upload(&n4, F.node4, K));
+  float* n4q;
+  RCHK(upload(&n4q, F.node4q, K));
   RCHK(upload(&tp, F.tri_pos, K));
   RCHK(upload(&ts, F.tri_shade, K));
   RCHK(upload(&md, F.media, K));
@@ -102,14 +104,20 @@ int renderer_create(const Scene& sc, int device, srr_renderer** out, std::string
   V.nodes = (const float4*)nodes;
   V.node4 = (const float4*)n4;
   V.node4_lds = (int)std::min<size_t>(kPathsLdsNodes, F.node4.size() / 32);
-  // Quad-cooperative mesh traversal pays once the BVH4 outgrows one XCD's 4 MB
-  // L2 (every node step then waits on the Infinity Cache / HBM, and a quad fetches
-  // a node's four children in parallel): measured 640,000-tri teapot 1,054 ->
-  // 1,573 Msamples/s, while the L2-resident C2/C4 meshes lose 13 % / 8 %.
-  // SRR_QUAD=0/1 forces either way.
+  V.node4q = F.node4q_ok && !F.node4q.empty() ? (const float4*)n4q : nullptr;
+  V.node4_lds_q = (int)std::min<size_t>(2 * kPathsLdsNodes, F.node4q.size() / kNode4qWords);
+  {  // compressed 64-B nodes for the per-lane mesh walks (SRR_CBVH=0/1)
+    const char* e = getenv("SRR_CBVH");
+    V.use_q = V.node4q && e && atoi(e) != 0;
+  }
+  // Quad-cooperative mesh traversal (SRR_QUAD=1; off by default).  In round 2 it
+  // paid on the 640,000-triangle teapot (1,054 -> 1,573 Msamples/s), but most of
+  // that came from sharing the whole-tree walks of NaN-bound rays over a quad;
+  // with those folded cooperatively (kernels.hip mesh_scan_nan) the per-lane walk
+  // is faster there too: 5,384 vs 5,170 Msamples/s.
   {
     const char* e = getenv("SRR_QUAD");
-    V.quad_trace = e ? (atoi(e) != 0) : (F.node4.size() * sizeof(float) > (4u << 20));
+    V.quad_trace = e ? (atoi(e) != 0) : false;
     const char* q = getenv("SRR_QUAD_MAX");
     V.quad_max = q ? atoi(q) : 32;  // 640k-tri teapot: 16 -> 1,569, 32 -> 1,598, 64 -> 1,552 Msamples/s
   }

@@ -849,6 +849,7 @@ struct Flattener {
       F.nodes.insert(F.nodes.end(), {n.box.mn[0], n.box.mn[1], n.box.mn[2], sf, n.box.mx[0], n.box.mx[1], n.box.mx[2], lf});
     }
     build_node4(B, m);
+    const size_t tri_first = F.tri_pos.size() / 16;
     for (int l : B.leaves) {
       const HTri& t = S.tris[S.obj[l].tri];
       for (int k = 0; k < 3; ++k) F.tri_pos.insert(F.tri_pos.end(), {t.p[3 * k], t.p[3 * k + 1], t.p[3 * k + 2], 0.f});
@@ -859,8 +860,110 @@ struct Flattener {
       sh.mat = t.mat;
       F.tri_shade.push_back(sh);
     }
+    build_node4q(m, tri_first);
     F.meshes.push_back(m);
     return mesh_of_bvh[h] = (int)F.meshes.size() - 1;
+  }
+
+  // Quantised bound on one axis: the smallest q with fl(o + q*s) <= v (lower) or
+  // the largest-needed q with fl(o + q*s) >= v (upper), in the device's float
+  // arithmetic (no contraction); false when 8 bits do not reach.
+  static bool quant(float o, float sc, float v, bool upper, uint32_t& q) {
+    if (!(v == v)) return false;
+    double g = ((double)v - (double)o) / (double)sc;
+    long long k = upper ? (long long)std::ceil(g) : (long long)std::floor(g);
+    k = std::max(0LL, std::min(255LL, k));
+    auto at = [&](long long x) {
+      volatile float d = (float)x * sc;  // (volatile: one float rounding per step, as on the device)
+      volatile float r = o + d;
+      return (float)r;
+    };
+    if (upper) {
+      while (k < 255 && at(k) < v) ++k;
+      if (at(k) < v) return false;
+    } else {
+      while (k > 0 && at(k) > v) --k;
+      if (at(k) > v) return false;
+    }
+    q = (uint32_t)k;
+    return true;
+  }
+
+  // The 64-B compressed copy of this mesh's 4-wide nodes (device_scene.h
+  // kNode4qWords).  A leaf child's exact box must be what the device recomputes
+  // from its 1-2 triangles (ffmin / ffmax of the vertices, triangle.h:53-68,
+  // bvh.h's surrounding_box): checked here; a mismatch (NaN vertices) turns the
+  // compressed nodes off for the scene.
+  void build_node4q(const DMesh& m, size_t tri_first) {
+    F.node4q.resize(F.node4.size() / 2, 0.f);
+    auto ffmin = [](float a, float b) { return a < b ? a : b; };
+    auto ffmax = [](float a, float b) { return a > b ? a : b; };
+    for (int ni = m.node4_off; ni < m.node4_off + m.n_node4; ++ni) {
+      const float* d = &F.node4[32 * (size_t)ni];
+      int32_t ch[4];
+      std::memcpy(ch, d + 24, 16);
+      float o[3], sc[3];
+      uint32_t q[6] = {0, 0, 0, 0, 0, 0};
+      for (int a = 0; a < 3; ++a) {
+        float lo = INFINITY, hi = -INFINITY;
+        for (int c = 0; c < 4; ++c)
+          if (ch[c] != INT32_MIN) {
+            lo = std::min(lo, d[4 * a + c]);
+            hi = std::max(hi, d[12 + 4 * a + c]);
+          }
+        if (!(lo <= hi)) { lo = hi = 0.f; }  // all-empty node (not built) or NaN: handled below
+        o[a] = lo;
+        // scale: a power of two with 255 steps covering the extent, at least an
+        // ulp-sized step of the coordinates
+        const float ext = hi - lo;
+        int e = -126;
+        if (ext > 0) e = std::max(e, (int)std::ceil(std::log2((double)ext / 250.0)));
+        const float mag = std::max(std::fabs(lo), std::fabs(hi));
+        if (mag > 0) e = std::max(e, std::ilogb(mag) - 23);
+        for (;; ++e) {
+          sc[a] = std::ldexp(1.0f, e);
+          bool ok = true;
+          uint32_t qlo = 0, qhi = 0;
+          for (int c = 0; c < 4 && ok; ++c) {
+            uint32_t bl = 255, bh = 0;  // empty slot: lo > hi
+            if (ch[c] != INT32_MIN)
+              ok = quant(o[a], sc[a], d[4 * a + c], false, bl) && quant(o[a], sc[a], d[12 + 4 * a + c], true, bh);
+            qlo |= bl << (8 * c);
+            qhi |= bh << (8 * c);
+          }
+          if (ok) {
+            q[a] = qlo;
+            q[3 + a] = qhi;
+            break;
+          }
+          if (e > 127) {
+            F.node4q_ok = false;
+            break;
+          }
+        }
+      }
+      // leaf children: the exact box the device recomputes must be the stored one
+      for (int c = 0; c < 4; ++c) {
+        if (ch[c] >= 0 || ch[c] == INT32_MIN) continue;
+        const int leaf = ~ch[c], first = leaf >> 1, count = (leaf & 1) + 1;
+        float mn[3], mx[3];
+        for (int t = 0; t < count; ++t) {
+          const float* p = &F.tri_pos[16 * (tri_first + (size_t)(first - m.tri_off + t))];
+          for (int a = 0; a < 3; ++a) {
+            const float tmn = ffmin(ffmin(p[a], p[4 + a]), p[8 + a]);
+            const float tmx = ffmax(ffmax(p[a], p[4 + a]), p[8 + a]);
+            mn[a] = t ? ffmin(mn[a], tmn) : tmn;
+            mx[a] = t ? ffmax(mx[a], tmx) : tmx;
+          }
+        }
+        for (int a = 0; a < 3; ++a)
+          if (std::memcmp(&mn[a], &d[4 * a + c], 4) || std::memcmp(&mx[a], &d[12 + 4 * a + c], 4)) F.node4q_ok = false;
+      }
+      float* w = &F.node4q[kNode4qWords * (size_t)ni];
+      for (int a = 0; a < 3; ++a) { w[a] = o[a]; w[3 + a] = sc[a]; }
+      std::memcpy(w + 6, q, 24);
+      std::memcpy(w + 12, ch, 16);
+    }
   }
 
   // bvh_node over other hitables: the same threaded BVH2 records as add_mesh,

@@ -126,6 +126,11 @@ struct Flat {
   std::vector<DMesh> meshes;
   std::vector<float> nodes;             // 2 float4 per node (lo, hi)
   std::vector<float> node4;             // 8 float4 per 4-wide node
+  // the same 4-wide nodes compressed to 64 B (device_scene.h kNode4qWords):
+  // child boxes quantised to 8 bits per bound against the node's own box,
+  // rounded outward; leaf boxes are recomputed exactly from the triangles
+  std::vector<float> node4q;
+  bool node4q_ok = true;                // every mesh's leaf boxes recompute exactly
   std::vector<float> tri_pos;           // float4 x4 per triangle (p0, p1, p2, pad)
   std::vector<TriShade> tri_shade;
   std::vector<DMedium> media;
