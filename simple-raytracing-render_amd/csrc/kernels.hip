@@ -2004,7 +2004,9 @@ SRR_D void camera_ray(const SceneView& S, int pix, int s_global, double sx, doub
   int j = ny - 1 - pix / nx;  // Raytracing_n.cpp:827-828 (SURVEY Q12 fix)
   uint64_t h = 0xcbf29ce484222325ULL ^ base_seed;
   uint32_t w[3] = {(uint32_t)i, (uint32_t)j, (uint32_t)s_global};
+#pragma unroll
   for (int k = 0; k < 3; ++k)
+#pragma unroll
     for (int b = 0; b < 4; ++b) {
       h ^= (w[k] >> (8 * b)) & 0xffu;
       h *= 0x100000001b3ULL;
