@@ -21,6 +21,7 @@ struct SceneView {  // device pointers into the flattened tables (device_scene.h
   const float4* nodes;  // 2 float4 per BVH2 node: lo (min.xyz, skip), hi (max.xyz, leaf)
   const float4* node4;  // 8 float4 per 4-wide node (device_scene.h), breadth-first per mesh
   int node4_lds;        // leading nodes the path kernel keeps in LDS (<= kPathsLdsNodes)
+  int node4_total;      // BVH4 nodes of all meshes (the LDS caches take a prefix)
   const float4* node4q; // the same nodes compressed to 64 B (device_scene.h kNode4qWords), or nullptr
   int node4_lds_q;      // ...and how many of those the path kernel keeps in LDS (<= 2 kPathsLdsNodes)
   int use_q;            // k_paths traces meshes over node4q (SRR_CBVH)
@@ -125,6 +126,7 @@ constexpr int kPathsWorldLdsBytes = 8192;  // == kernels.hip kWorldLdsBytes
 constexpr int kPathsLdsNodes = SRR_LDS_NODES;  // BVH4 nodes cached in LDS by k_paths (128 B each)
 void dump_trace_timing();
 int paths_lanes_per_device(const SceneView& S, int device);  // persistent grid capacity
+int paths_block_lanes(const SceneView& S);  // k_paths lanes per block for this scene (256 or 1,024)
 void launch_paths(const SceneView& S, const PathWork& W, int all_families, hipStream_t st);
 // device known-answer tests (srr_device_kat); kind = dev::KatKind
 // device tables of the camera / light KATs (srr_device_kat builds them with the

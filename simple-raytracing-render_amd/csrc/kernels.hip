@@ -342,7 +342,7 @@ SRR_D float q_bound(float o, float s, uint32_t w, int c) { return o + (float)((w
 // exact box, recomputed from the leaf's 1-2 triangles (ffmin / ffmax of the
 // vertices: the reference's triangle / bvh_node box, triangle.h:53-68) with the
 // reference's slab arithmetic -- the same leaf set as the 128-B nodes.
-template <bool PRUNE, bool TIMING = false, bool Q = false>
+template <bool PRUNE, bool TIMING = false, bool Q = false, int STRIDE = kTraceBlock>
 SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmin, float tmax, bool is_medium,
                      MeshHit& out, const TraceCtx& cx) {
   if (const uint64_t nanm = __ballot(!(tmax == tmax))) {  // NaN bound: the fold over all triangles
@@ -491,8 +491,8 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
       for (int c = 3; c >= 1; --c) {
         if (kn[c] < 0) continue;
         if (sp < cx.st_cap) {
-          cx.st_node[sp * kTraceBlock] = kn[c];
-          cx.st_t[sp * kTraceBlock] = kt[c];
+          cx.st_node[sp * STRIDE] = kn[c];
+          cx.st_t[sp * STRIDE] = kt[c];
           ++sp;
         } else if (sp < cx.st_cap + cx.gst_cap) {
           cx.gst[(size_t)(sp - cx.st_cap) * cx.gst_stride + cx.slot] = make_int2(kn[c], __float_as_int(kt[c]));
@@ -511,8 +511,8 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
       int cand;
       float ct;
       if (sp < cx.st_cap) {
-        cand = cx.st_node[sp * kTraceBlock];
-        ct = cx.st_t[sp * kTraceBlock];
+        cand = cx.st_node[sp * STRIDE];
+        ct = cx.st_t[sp * STRIDE];
       } else {
         const int2 e = cx.gst[(size_t)(sp - cx.st_cap) * cx.gst_stride + cx.slot];
         cand = e.x;
@@ -569,6 +569,8 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
 // whose stack overflows leaves its ray to the exact BVH2 re-walk.
 constexpr int TR_QUAD = 32;
 constexpr int TR_Q = 64;  // meshes traced over the compressed 64-B nodes (SceneView::node4q)
+constexpr int TR_BIG = 128;  // the 1,024-lane path kernel: LDS stacks with stride 1,024
+constexpr int tr_stride(int tr) { return (tr & TR_BIG) ? 1024 : kTraceBlock; }
 
 template <int CTRL>
 SRR_D int quad_dpp(int x) { return __builtin_amdgcn_update_dpp(x, x, CTRL, 0xF, 0xF, false); }
@@ -591,7 +593,7 @@ SRR_D void quad_best(bool& f, float& t, int& i) {
 #undef SRR_QSTEP
 }
 
-template <bool PRUNE>
+template <bool PRUNE, int STRIDE = kTraceBlock>
 SRR_D bool mesh_hit4_quad(const SceneView& S, const DMesh& m, const Ray& r, float tmin, float tmax, bool is_medium,
                           MeshHit& out, const TraceCtx& cx) {
   if (const uint64_t nanm = __ballot(!(tmax == tmax))) {  // NaN bound: the fold over all triangles (mesh_scan_nan)
@@ -614,13 +616,13 @@ SRR_D bool mesh_hit4_quad(const SceneView& S, const DMesh& m, const Ray& r, floa
   const bool want = slab(S.nodes[2 * m.node_off], S.nodes[2 * m.node_off + 1], r.o, inv, tmin, tmax);
   if (__ballot(1) != ~0ull) {  // not a full wave (its last paths): per lane
     if (!want) return false;
-    return mesh_hit4<PRUNE>(S, m, r, tmin, tmax, is_medium, out, cx);
+    return mesh_hit4<PRUNE, false, false, STRIDE>(S, m, r, tmin, tmax, is_medium, out, cx);
   }
   const int lane = __lane_id(), q = lane >> 2, c = lane & 3;
   const float len = length(r.d);
   const V3 dir = r.d / len;
   const float to_param = kPruneSlack / len;
-  // quad lane 0's stacks serve its quad (entry e of lane l - c is cx.st_*[e * kTraceBlock - c])
+  // quad lane 0's stacks serve its quad (entry e of lane l - c is cx.st_*[e * STRIDE - c])
   const int gslot = cx.slot - c;
   bool found_me = false, redo_me = false;
   float t_me = 0;
@@ -628,7 +630,7 @@ SRR_D bool mesh_hit4_quad(const SceneView& S, const DMesh& m, const Ray& r, floa
   uint64_t W = __ballot(want);
   if (__popcll(W) > S.quad_max) {  // many rays enter: one per lane
     if (!want) return false;
-    return mesh_hit4<PRUNE>(S, m, r, tmin, tmax, is_medium, out, cx);
+    return mesh_hit4<PRUNE, false, false, STRIDE>(S, m, r, tmin, tmax, is_medium, out, cx);
   }
   while (W) {
     // this round: up to 16 wanting lanes, quad k serving the k-th
@@ -728,8 +730,8 @@ SRR_D bool mesh_hit4_quad(const SceneView& S, const DMesh& m, const Ray& r, floa
           if (take && rank > 0) {  // pushed farthest first: rank 1 ends on top
             const int pos = sp + (ntake - 1 - rank);
             if (pos < cx.st_cap) {
-              cx.st_node[pos * kTraceBlock - c] = ch;
-              cx.st_t[pos * kTraceBlock - c] = lo_;
+              cx.st_node[pos * STRIDE - c] = ch;
+              cx.st_t[pos * STRIDE - c] = lo_;
             } else if (pos < cx.st_cap + cx.gst_cap) {
               cx.gst[(size_t)(pos - cx.st_cap) * cx.gst_stride + gslot] = make_int2(ch, __float_as_int(lo_));
               deep = true;
@@ -746,8 +748,8 @@ SRR_D bool mesh_hit4_quad(const SceneView& S, const DMesh& m, const Ray& r, floa
             int cand;
             float ctt;
             if (sp < cx.st_cap) {
-              cand = cx.st_node[sp * kTraceBlock - c];
-              ctt = cx.st_t[sp * kTraceBlock - c];
+              cand = cx.st_node[sp * STRIDE - c];
+              ctt = cx.st_t[sp * STRIDE - c];
             } else {
               const int2 e = cx.gst[(size_t)(sp - cx.st_cap) * cx.gst_stride + gslot];
               cand = e.x;
@@ -925,9 +927,13 @@ SRR_D bool basic_hit(const SceneView& S, const DObj& ob, const Ray& lr, float tm
       const DMesh m = wload<TR>(S.meshes, ob.idx);
       bool hit;
       if (tr_mode(TR) == TR_BVH2) hit = mesh_hit<false>(S, m, lr, tmin, tmax, is_medium, mh, cx.ctr);
-      else if (TR & TR_QUAD) hit = mesh_hit4_quad<tr_mode(TR) != TR_BVH4>(S, m, lr, tmin, tmax, is_medium, mh, cx);
-      else if (TR & TR_Q) hit = mesh_hit4<tr_mode(TR) != TR_BVH4, false, true>(S, m, lr, tmin, tmax, is_medium, mh, cx);
-      else hit = mesh_hit4<tr_mode(TR) != TR_BVH4, tr_mode(TR) == TR_BVH4_TIMED>(S, m, lr, tmin, tmax, is_medium, mh, cx);
+      else if (TR & TR_QUAD)
+        hit = mesh_hit4_quad<tr_mode(TR) != TR_BVH4, tr_stride(TR)>(S, m, lr, tmin, tmax, is_medium, mh, cx);
+      else if (TR & TR_Q)
+        hit = mesh_hit4<tr_mode(TR) != TR_BVH4, false, true, tr_stride(TR)>(S, m, lr, tmin, tmax, is_medium, mh, cx);
+      else
+        hit = mesh_hit4<tr_mode(TR) != TR_BVH4, tr_mode(TR) == TR_BVH4_TIMED, false, tr_stride(TR)>(
+            S, m, lr, tmin, tmax, is_medium, mh, cx);
       if (!hit) return false;
       h.t = mh.t;
       h.prim = mh.tri;
@@ -2373,10 +2379,17 @@ constexpr unsigned long long kPoolChunk = 64;  // path indices a wave takes per 
 // result of every ray is mesh_hit4's, so paths stay bit-identical.
 constexpr int kPathsLdsNodesCmp = 56;  // LDS node cache of the CMP variant (room for the queue)
 
+// BS: lanes per block.  256 (4 blocks per CU) or 1,024 (one block per CU, the same
+// 4 waves per SIMD): one LDS allocation per CU, whose 160 KB then cache
+// kPathsLdsNodesBig BVH4 nodes (the top ~5 levels) instead of 96.
+constexpr int kPathsLdsNodesBig = 696;  // 8 KB world + 64 KB stacks + 696 x 128 B < 160 KB
+
 template <bool MEDIA, bool ALLFAM, int MINB, bool TIMED = false, bool WL = true, bool QUAD = false, bool CMP = false,
-          bool CQ = false>
-__global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathWork W) {
-  static_assert(!CMP || (!MEDIA && !TIMED && WL && !QUAD), "CMP: world list in LDS, no media, per-lane walks");
+          bool CQ = false, int BS = kPathsBlock>
+__global__ void __launch_bounds__(BS, MINB) k_paths(SceneView S0, PathWork W) {
+  static_assert(!CMP || (!MEDIA && !TIMED && WL && !QUAD && BS == kPathsBlock),
+                "CMP: world list in LDS, no media, per-lane walks, 256-lane blocks");
+  static_assert(BS == kPathsBlock || BS == 1024, "block size");
   // TIMED (diagnostics): per-wave cycles in refill / world hit (mesh part) / record+scatter / fold
   uint64_t tp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t it = 0;
@@ -2385,7 +2398,7 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
   // WL: world tables staged in LDS (they fit in kWorldLdsBytes); otherwise read
   // from global memory (large object lists, e.g. random_scene's ~490 spheres)
   // QUAD: meshes traced by mesh_hit4_quad (large BVHs, SceneView::quad_trace)
-  constexpr int TR = TR_BVH4_PRUNE | (WL ? TR_WL : 0) | (QUAD ? TR_QUAD : 0) | (CQ ? TR_Q : 0);
+  constexpr int TR = TR_BVH4_PRUNE | (WL ? TR_WL : 0) | (QUAD ? TR_QUAD : 0) | (CQ ? TR_Q : 0) | (BS == 1024 ? TR_BIG : 0);
   if constexpr (WL) {
     __shared__ uint4 s_world[kWorldLdsBytes / 16];
     for (int i = threadIdx.x; i < S0.world_words; i += blockDim.x) s_world[i] = S0.world_blob[i];
@@ -2402,11 +2415,11 @@ __global__ void __launch_bounds__(kPathsBlock, MINB) k_paths(SceneView S0, PathW
     S.texs = (const DTex*)(b + S0.world_off[8]);
     S.lights = (const DLight*)(b + S0.world_off[9]);
   }
-  __shared__ int s_node[kStack * kPathsBlock];
-  __shared__ float s_t[kStack * kPathsBlock];
-  constexpr int kNodesLds = CMP ? kPathsLdsNodesCmp : kPathsLdsNodes;
+  __shared__ int s_node[kStack * BS];
+  __shared__ float s_t[kStack * BS];
+  constexpr int kNodesLds = CMP ? kPathsLdsNodesCmp : (BS == 1024 ? kPathsLdsNodesBig : kPathsLdsNodes);
   // (CQ: the same LDS bytes hold twice as many 64-B nodes)
-  const int n_lds_nodes = CQ ? min(S0.node4_lds_q, 2 * kNodesLds) : min(S0.node4_lds, kNodesLds);
+  const int n_lds_nodes = CQ ? min(S0.node4_total, 2 * kNodesLds) : min(S0.node4_total, kNodesLds);
   __shared__ float4 s_n4[kNodesLds * 8];
   if (CQ)
     for (int i = threadIdx.x; i < n_lds_nodes * 4; i += blockDim.x) s_n4[i] = S0.node4q[i];
@@ -3290,6 +3303,26 @@ static int paths_min_blocks() {
   return v;
 }
 
+// Lanes per k_paths block for this scene: 1,024 (SRR_BIGBLOCK, the default) when the
+// launch would take the per-lane, LDS-world path, else 256.  render_paths rounds
+// the window's lanes to it.
+int paths_block_lanes(const SceneView& S) {
+  static const bool big = [] {
+    const char* e = getenv("SRR_BIGBLOCK");
+    return !e || atoi(e) != 0;
+  }();
+  static const bool timed = getenv("SRR_PATHS_TIMING") != nullptr;
+  static const bool force_global = getenv("SRR_WORLD_GLOBAL") != nullptr;
+  static const bool compact = [] {
+    const char* e = getenv("SRR_COMPACT");
+    return e && atoi(e) != 0;
+  }();
+  const bool wl = !force_global && S.world_words * 16 <= dev::kWorldLdsBytes;
+  const bool cmp = compact && S.mesh_obj >= 0 && !S.has_media && !S.quad_trace;
+  return (big && wl && !timed && !cmp && !S.quad_trace && paths_min_blocks() == kPathsOccDefault) ? 1024
+                                                                                                    : dev::kPathsBlock;
+}
+
 int paths_lanes_per_device(const SceneView& S, int device) {
   (void)S;
   int cus = 0, per_cu = 0;
@@ -3326,9 +3359,13 @@ void launch_paths(const SceneView& S, const PathWork& W, int all_families, hipSt
   }();
   const bool cmp = compact && S.mesh_obj >= 0 && !S.has_media && !S.quad_trace && !timed;
   const bool cq = S.use_q && !S.quad_trace && !timed && !cmp;  // compressed nodes, per-lane walks
+  const int bs = paths_block_lanes(S);
+  const int blocks_b = W.lanes / bs;
 #define SRR_LAUNCH_PATHS(M, A, B)                                                                      \
   if (timed) hipLaunchKernelGGL((dev::k_paths<M, A, 4, true>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W); \
   else if (!M && cmp && B == 4) hipLaunchKernelGGL((dev::k_paths<false, A, 4, false, true, false, true>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W); \
+  else if (bs == 1024 && B == 4 && cq) hipLaunchKernelGGL((dev::k_paths<M, A, 4, false, true, false, false, true, 1024>), dim3(blocks_b), dim3(1024), 0, st, S, W); \
+  else if (bs == 1024 && B == 4 && !S.quad_trace) hipLaunchKernelGGL((dev::k_paths<M, A, 4, false, true, false, false, false, 1024>), dim3(blocks_b), dim3(1024), 0, st, S, W); \
   else if (cq && B == 4) hipLaunchKernelGGL((dev::k_paths<M, A, 4, false, true, false, false, true>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W); \
   else if (S.quad_trace && B == 4) hipLaunchKernelGGL((dev::k_paths<M, A, 4, false, true, true>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W); \
   else hipLaunchKernelGGL((dev::k_paths<M, A, B>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W)

@@ -104,6 +104,7 @@ int renderer_create(const Scene& sc, int device, srr_renderer** out, std::string
   V.nodes = (const float4*)nodes;
   V.node4 = (const float4*)n4;
   V.node4_lds = (int)std::min<size_t>(kPathsLdsNodes, F.node4.size() / 32);
+  V.node4_total = (int)(F.node4.size() / 32);
   V.node4q = F.node4q_ok && !F.node4q.empty() ? (const float4*)n4q : nullptr;
   V.node4_lds_q = (int)std::min<size_t>(2 * kPathsLdsNodes, F.node4q.size() / kNode4qWords);
   {  // compressed 64-B nodes for the per-lane mesh walks (SRR_CBVH=0/1)
@@ -434,7 +435,8 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
     w.keep_s0 = s0;
     w.rec = r->pw_rec;
     w.err = (int*)(r->pw_ctr + 2);
-    w.lanes = (int)std::min<int64_t>(r->pw_lanes, ((w.n_paths + 255) / 256) * 256);
+    const int64_t bl = paths_block_lanes(r->view);  // whole blocks of the launch's size
+    w.lanes = (int)std::min<int64_t>(r->pw_lanes, ((w.n_paths + bl - 1) / bl) * bl);
     w.stack_cap = kPathsLdsStack;  // kernels.hip kStack
     if (const char* e = getenv("SRR_STACK_CAP")) w.stack_cap = std::max(1, std::min(kPathsLdsStack, atoi(e)));
     w.gstack = gst_cap ? r->pw_gstack : nullptr;
