@@ -342,6 +342,11 @@ SRR_D float q_bound(float o, float s, uint32_t w, int c) { return o + (float)((w
 // exact box, recomputed from the leaf's 1-2 triangles (ffmin / ffmax of the
 // vertices: the reference's triangle / bvh_node box, triangle.h:53-68) with the
 // reference's slab arithmetic -- the same leaf set as the 128-B nodes.
+#ifndef SRR_LEAFQ
+#define SRR_LEAFQ 1
+#endif
+constexpr bool LEAFQ = SRR_LEAFQ != 0;  // mesh_hit4's leaf-triangle queue (A/B: -DSRR_LEAFQ=0)
+
 template <bool PRUNE, bool TIMING = false, bool Q = false, int STRIDE = kTraceBlock>
 SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmin, float tmax, bool is_medium,
                      MeshHit& out, const TraceCtx& cx) {
@@ -427,6 +432,53 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
 #undef SRR_SLAB_AX
 #undef SRR_CHILD
     const int ch[4] = {CH.x, CH.y, CH.z, CH.w};
+    if constexpr (!Q && LEAFQ) {
+      // The leaf children this step hit, as a queue of (leaf, triangle) work: one
+      // pass of the loop tests one triangle of every lane that has one, whatever
+      // child slot its leaves sit in (slot by slot, a wave ran the triangle test
+      // once per slot with a leaf, each time for a few lanes).  The fold is
+      // order-free (`wins`), and the bound may only shrink: the same result.
+      int q0 = -1, q1 = -1, q2 = -1, q3 = -1;  // leaf codes ~child, in slot order
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        // (a NaN ray passes every slab test, as in the reference, so empty slots
+        // are told apart by their INT_MIN child, not by their inverted box)
+        if (!hit[c] || ch[c] >= 0 || ch[c] == INT32_MIN) continue;
+        const int leaf = ~ch[c];
+        ntri += 2;
+        if (q0 < 0) q0 = leaf;
+        else if (q1 < 0) q1 = leaf;
+        else if (q2 < 0) q2 = leaf;
+        else q3 = leaf;
+      }
+      int sub = 0;  // triangle of leaf q0 under test
+      while (q0 >= 0) {
+        const int ti = (q0 >> 1) + sub;
+        const float4* tp = S.tri_pos + kTriStride * (size_t)ti;
+        const float4 a = tp[0], b = tp[1], cc = tp[2];
+        const V3 p0 = v3(a.x, a.y, a.z), p1 = v3(b.x, b.y, b.z), p2 = v3(cc.x, cc.y, cc.z);
+        float t, u, v;
+        bool h = tri_hit(p0, p1, p2, true, r.o, dir, t, u, v);
+        if (!h && is_medium) h = tri_hit(p0, p1, p2, false, r.o, dir, t, u, v);
+        if (h && (!found || wins(t, ti, best_t, best_i))) {
+          found = true;
+          best_t = t;
+          best_i = ti;
+        }
+        // shrink only with ordered compares: a NaN bound (the reference passes
+        // every box then) or a NaN best keeps the bound as it is
+        if (PRUNE && found && best_t * to_param < bound) bound = best_t * to_param;
+        if (sub == 0 && (q0 & 1)) {
+          sub = 1;
+        } else {
+          sub = 0;
+          q0 = q1;
+          q1 = q2;
+          q2 = q3;
+          q3 = -1;
+        }
+      }
+    } else
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       // (a NaN ray passes every slab test, as in the reference, so empty slots
