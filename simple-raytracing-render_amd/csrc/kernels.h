@@ -82,6 +82,18 @@ struct BatchInfo {
   uint64_t base_seed;
 };
 
+// floor(n / d) for 0 <= n < 2^31 as (n * m) >> p with m = ceil(2^p / d),
+// p = 31 + ceil(log2 d) (Granlund-Montgomery: exact for every 31-bit n; m < 2^32)
+struct UDiv31 {
+  uint32_t m, p;
+};
+inline UDiv31 make_udiv31(uint32_t d) {
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  const uint32_t p = 31 + l;
+  return UDiv31{(uint32_t)(((1ull << p) + d - 1) / d), p};
+}
+
 // One window of a frame for the path-resident persistent kernel (k_paths):
 // every (pixel, sample) of pixels x [0, spp_w) is a path, numbered pixel-major
 // g = lp * spp_w + s (a wave's lanes take samples of one pixel: coherent first
@@ -92,6 +104,7 @@ struct PathWork {
   int npix, spp_w;
   int s_base;             // global sample index of window sample 0 (per-path seeds)
   int nx, ny;
+  UDiv31 div_spp, div_nx;  // invariant divisors spp_w and nx (path index -> pixel, pixel -> i, j)
   uint64_t base_seed;
   int64_t n_paths;        // npix * spp_w
   int max_depth;

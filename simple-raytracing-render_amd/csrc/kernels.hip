@@ -346,6 +346,9 @@ SRR_D float q_bound(float o, float s, uint32_t w, int c) { return o + (float)((w
 #define SRR_LEAFQ 1
 #endif
 constexpr bool LEAFQ = SRR_LEAFQ != 0;  // mesh_hit4's leaf-triangle queue (A/B: -DSRR_LEAFQ=0)
+#ifndef SRR_TRIPF
+#define SRR_TRIPF 1
+#endif
 
 template <bool PRUNE, bool TIMING = false, bool Q = false, int STRIDE = kTraceBlock>
 SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmin, float tmax, bool is_medium,
@@ -452,10 +455,30 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
         else q3 = leaf;
       }
       int sub = 0;  // triangle of leaf q0 under test
+#if SRR_TRIPF
+      // software pipelined: the next triangle's vertices are in flight while
+      // this one is tested (one L2 / Infinity Cache latency per pass, not two)
+      float4 na{}, nb{}, nc{};
+      if (q0 >= 0) {
+        const float4* tp = S.tri_pos + kTriStride * (size_t)(q0 >> 1);
+        na = tp[0], nb = tp[1], nc = tp[2];
+      }
+#endif
       while (q0 >= 0) {
         const int ti = (q0 >> 1) + sub;
+#if SRR_TRIPF
+        const float4 a = na, b = nb, cc = nc;
+        {
+          const int nti = (sub == 0 && (q0 & 1)) ? ti + 1 : (q1 >= 0 ? (q1 >> 1) : -1);
+          if (nti >= 0) {
+            const float4* tp = S.tri_pos + kTriStride * (size_t)nti;
+            na = tp[0], nb = tp[1], nc = tp[2];
+          }
+        }
+#else
         const float4* tp = S.tri_pos + kTriStride * (size_t)ti;
         const float4 a = tp[0], b = tp[1], cc = tp[2];
+#endif
         const V3 p0 = v3(a.x, a.y, a.z), p1 = v3(b.x, b.y, b.z), p2 = v3(cc.x, cc.y, cc.z);
         float t, u, v;
         bool h = tri_hit(p0, p1, p2, true, r.o, dir, t, u, v);
@@ -1144,6 +1167,7 @@ SRR_D void sphere_uv(V3 p, float& u, float& v) {  // hitable.h:10-15
 }
 
 // record of one primitive (or mesh triangle `prim`) hit at t, in its local frame
+template <int TR = 0>
 SRR_D void prim_record(const SceneView& S, const DObj& ob, const Ray& lr, float t, int prim, HitRec& h) {
   switch (ob.kind) {
     case OBJ_SPHERE:
@@ -1168,22 +1192,36 @@ SRR_D void prim_record(const SceneView& S, const DObj& ob, const Ray& lr, float 
     }
     case OBJ_TRI:
     case OBJ_MESH: {
+      // (values, not a pointer into either table: a pointer that may be LDS or
+      // global compiles to flat loads, whose waits drain both the vector-memory
+      // and the LDS counters)
       V3 p0, p1, p2;
-      const TriShade* sh;
+      TriShade shv;
       if (ob.kind == OBJ_TRI) {
-        const DStandaloneTri& T = S.stris[ob.idx];
+        DStandaloneTri T;
+        if constexpr ((TR & TR_WL) != 0) {  // world tables in LDS: LDS-space loads
+          static_assert(sizeof(DStandaloneTri) == 25 * 4, "DStandaloneTri: 25 words");
+          const __attribute__((address_space(3))) float* q =
+              (const __attribute__((address_space(3))) float*)(S.stris + ob.idx);
+          float* t = (float*)&T;
+#pragma unroll
+          for (int k = 0; k < 25; ++k) t[k] = q[k];
+        } else {
+          T = S.stris[ob.idx];
+        }
         p0 = v3(T.p[0], T.p[1], T.p[2]);
         p1 = v3(T.p[3], T.p[4], T.p[5]);
         p2 = v3(T.p[6], T.p[7], T.p[8]);
-        sh = &T.sh;
+        shv = T.sh;
       } else {
         const float4* tp = S.tri_pos + kTriStride * (size_t)prim;
         float4 a = tp[0], b = tp[1], c = tp[2];
         p0 = v3(a.x, a.y, a.z);
         p1 = v3(b.x, b.y, b.z);
         p2 = v3(c.x, c.y, c.z);
-        sh = &S.tri_shade[prim];
+        shv = S.tri_shade[prim];
       }
+      const TriShade* sh = &shv;
       V3 dir = lr.d / length(lr.d);
       float tt, u, v;
       tri_hit(p0, p1, p2, true, lr.o, dir, tt, u, v);  // world rays never take the back test
@@ -1218,10 +1256,10 @@ SRR_D HitRec world_record(const SceneView& S, const Ray& r, const WorldHit& w) {
   h.v = 0;  // defined here as 0
   if (ob.kind == OBJ_OBVH) {  // the primitive inside the object BVH, then the node's chain
     const DObj& in = S.objs[w.prim];
-    prim_record(S, in, chain_in<TR>(S, in, lr), w.t, -1, h);
+    prim_record<TR>(S, in, chain_in<TR>(S, in, lr), w.t, -1, h);
     chain_out(S, in, h.p, h.n);
   } else {
-    prim_record(S, ob, lr, w.t, w.prim, h);
+    prim_record<TR>(S, ob, lr, w.t, w.prim, h);
   }
   chain_out(S, ob, h.p, h.n);
   return h;
@@ -2056,10 +2094,13 @@ SRR_D void sobol2_point(uint32_t i, double& sx, double& sy) {
 
 // The camera ray of sample s_global of pixel `pix` with its per-path RNG streams
 // (SURVEY §8(d) seeding; Raytracing_n.cpp:827-836; camera::get_ray, camera.h:51-59).
+SRR_D uint32_t udiv31(uint32_t n, UDiv31 v) { return (uint32_t)(((uint64_t)n * v.m) >> v.p); }
+
 SRR_D void camera_ray(const SceneView& S, int pix, int s_global, double sx, double sy, int nx, int ny,
-                      uint64_t base_seed, V3& o, V3& dir, float& time, Rng& rng) {
-  int i = pix % nx;
-  int j = ny - 1 - pix / nx;  // Raytracing_n.cpp:827-828 (SURVEY Q12 fix)
+                      uint64_t base_seed, V3& o, V3& dir, float& time, Rng& rng, const UDiv31* dnx = nullptr) {
+  const int q = dnx ? (int)udiv31((uint32_t)pix, *dnx) : pix / nx;
+  int i = pix - q * nx;   // pix % nx
+  int j = ny - 1 - q;     // Raytracing_n.cpp:827-828 (SURVEY Q12 fix)
   uint64_t h = 0xcbf29ce484222325ULL ^ base_seed;
   uint32_t w[3] = {(uint32_t)i, (uint32_t)j, (uint32_t)s_global};
 #pragma unroll
@@ -2498,6 +2539,12 @@ __global__ void __launch_bounds__(BS, MINB) k_paths(SceneView S0, PathWork W) {
   uint32_t pool = 0, pool_end = 0;
   uint32_t nxt_lane0 = 0;  // lane 0: base of the armed next chunk
   bool nxt_armed = false;
+  // the armed chunk's base, read once the world hit is done (nxt_ready): by then
+  // the atomic has long returned, and no store of this iteration is yet in flight
+  // (the wave's vector-memory counter is in issue order, so reading the atomic's
+  // result right after the fold's sample stores would wait for those)
+  uint32_t nxt_base = 0;
+  bool nxt_ready = false;
   Ray r{};
   Rng rng{};
   int depth = 0;
@@ -2523,8 +2570,9 @@ __global__ void __launch_bounds__(BS, MINB) k_paths(SceneView S0, PathWork W) {
       } else {
         uint32_t nb;
         if (nxt_armed) {
-          nb = __builtin_amdgcn_readfirstlane(nxt_lane0);
+          nb = nxt_ready ? nxt_base : __builtin_amdgcn_readfirstlane(nxt_lane0);
           nxt_armed = false;
+          nxt_ready = false;
         } else {
           uint32_t b = 0;
           if (lane_id() == 0) b = (uint32_t)atomicAdd(W.cursor, (unsigned long long)kPoolChunk);
@@ -2537,14 +2585,14 @@ __global__ void __launch_bounds__(BS, MINB) k_paths(SceneView S0, PathWork W) {
       if (need && idx < n_paths) {
         g = (int)idx;
         // pixel-major: g = lp * spp_w + s
-        const uint32_t lp = idx / (uint32_t)W.spp_w, s = idx - lp * (uint32_t)W.spp_w;
+        const uint32_t lp = udiv31(idx, W.div_spp), s = idx - lp * (uint32_t)W.spp_w;
         if ((int)lp >= W.npix || (int)s >= W.spp_w) atomicOr(W.err, 1);
         const int pix = W.pixels ? W.pixels[lp] : lp;
         V3 o, d;
         float tm;
         double sx, sy;
         sobol2_point((uint32_t)(W.s_base + (int)s), sx, sy);  // = W.sobol[2 s], W.sobol[2 s + 1]
-        camera_ray(S, pix, W.s_base + s, sx, sy, W.nx, W.ny, W.base_seed, o, d, tm, rng);
+        camera_ray(S, pix, W.s_base + s, sx, sy, W.nx, W.ny, W.base_seed, o, d, tm, rng, &W.div_nx);
         r = Ray{o, d, tm};
         depth = 0;
       }
@@ -2677,6 +2725,12 @@ __global__ void __launch_bounds__(BS, MINB) k_paths(SceneView S0, PathWork W) {
         tq = t;
       }
       done = true;
+    }
+    if (nxt_armed && !nxt_ready) {  // (uniform: every lane of the wave is here)
+      nxt_base = __builtin_amdgcn_readfirstlane(nxt_lane0);
+      nxt_ready = true;
+    }
+    if (g >= 0) {
       if (w.obj >= 0) {
         const HitRec h = world_record<TR>(S, r, w);
         const int kind = h.mat >= 0 ? S.mats[h.mat].kind : -1;

@@ -423,6 +423,8 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
     w.s_base = p->sample_begin + s0;
     w.nx = p->nx;
     w.ny = p->ny;
+    w.div_spp = make_udiv31((uint32_t)Wn);
+    w.div_nx = make_udiv31((uint32_t)p->nx);
     w.base_seed = p->base_seed;
     w.n_paths = (int64_t)npix * Wn;
     w.max_depth = p->max_depth;
