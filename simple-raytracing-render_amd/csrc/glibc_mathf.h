@@ -41,26 +41,12 @@ namespace gm {
 
 #include "glibc_mathf_tables.inc"
 
-GM_FN uint32_t asuint(float f) {
-  uint32_t u;
-  std::memcpy(&u, &f, 4);
-  return u;
-}
-GM_FN float asfloat(uint32_t u) {
-  float f;
-  std::memcpy(&f, &u, 4);
-  return f;
-}
-GM_FN uint64_t asuint64(double f) {
-  uint64_t u;
-  std::memcpy(&u, &f, 8);
-  return u;
-}
-GM_FN double asdouble(uint64_t u) {
-  double f;
-  std::memcpy(&f, &u, 8);
-  return f;
-}
+// (__builtin_bit_cast, not std::memcpy: on the device HIP's memcpy is a 4-byte
+// loop through scratch memory, which the register allocator kept in k_paths)
+GM_FN uint32_t asuint(float f) { return __builtin_bit_cast(uint32_t, f); }
+GM_FN float asfloat(uint32_t u) { return __builtin_bit_cast(float, u); }
+GM_FN uint64_t asuint64(double f) { return __builtin_bit_cast(uint64_t, f); }
+GM_FN double asdouble(uint64_t u) { return __builtin_bit_cast(double, u); }
 GM_FN uint32_t top12(float x) { return asuint(x) >> 20; }
 
 // e_expf.c: exp(x) = 2^(k/32) * 2^(r/32), k = round(x * 32/ln2)
