@@ -2024,6 +2024,7 @@ SRR_D bool bsdf_dead(const SceneView& S, const Bsdf& f, V3 p) {
     } else if (L.kind == LIGHT_TRI) {
       const DStandaloneTri T = S.stris[L.idx];
       float cs = 0;
+#pragma unroll
       for (int k2 = 0; k2 < 9; ++k2) cs = fmaxf(cs, fabsf(T.p[k2]));
       const float m = 1e-3f * (ps + cs);
       for (int c = 0; c < 3; ++c)

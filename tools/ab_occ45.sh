@@ -5,5 +5,5 @@ set -o pipefail
 L=$PWD/simple-raytracing-render_amd
 for sc in "--scene s4 --steps 2" "--scene s5 --spp 512 --steps 2"; do
   BENCH_ARGS="$sc" bash tools/ab_libs.sh occ$(echo $sc | cut -c9-10) \
-    "occ4:SRR_LIB=$L/exp_occ.so;SRR_BIGBLOCK=0" "occ3:SRR_LIB=$L/exp_occ.so;SRR_PATHS_OCC=3" "big:X=0" || exit 1
+    "occ4:SRR_LIB=$L/exp_occ.so;SRR_BIGBLOCK=0" "occ5:SRR_LIB=$L/exp_occ.so;SRR_PATHS_OCC=5" "occ6:SRR_LIB=$L/exp_occ.so;SRR_PATHS_OCC=6" || exit 1
 done

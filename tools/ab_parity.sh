@@ -1,6 +1,6 @@
 #!/bin/bash
 # parity subset on the default build, then A/B default vs LIB on C1, C2, C4 (run via gpurun)
-#   bash tools/ab_r3c.sh TAG LIB [LIB2]
+#   bash tools/ab_parity.sh TAG LIB [LIB2]
 set -o pipefail
 TAG=$1; L=$PWD/simple-raytracing-render_amd; O=gpurun_out
 if [ -z "$SKIP_TESTS" ]; then

@@ -9,7 +9,7 @@ import sys
 
 PKG = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "simple-raytracing-render_amd")
 cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-std=c++17", "-O3", "-fPIC", "-ffp-contract=off",
-       "-mllvm", "-disable-machine-licm", "-fno-slp-vectorize", "-fno-unroll-loops", *os.environ.get("EXTRA_HIPFLAGS", "").split(), "-c", "csrc/kernels.hip",
+       "-mllvm", "-disable-machine-licm", "-mllvm", "-amdgpu-atomic-optimizer-strategy=None", "-fno-slp-vectorize", "-fno-unroll-loops", *os.environ.get("EXTRA_HIPFLAGS", "").split(), "-c", "csrc/kernels.hip",
        "-o", "/dev/null", "-Rpass-analysis=kernel-resource-usage"]
 out = subprocess.run(cmd, cwd=PKG, capture_output=True, text=True).stderr
 flt = sys.argv[1] if len(sys.argv) > 1 else "k_paths"
