@@ -55,6 +55,10 @@ def parse():
                     help="multi-GPU split: tiles = strong scaling, the north_star split (one frame, --tile tiles "
                          "round-robin, one gather to rank 0; bitwise the 1-GPU image), samples = weak scaling "
                          "(each GPU renders spp samples of every pixel, one reduce of raw sums)")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="one frame at a time (srr_render_device) instead of two in flight "
+                         "(srr_render_device_async: frame k+1's persistent blocks start on the CUs frame k's last "
+                         "paths free, and frame k's exchange runs while frame k+1 renders)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--count-visits", action="store_true", help="diagnostic: count mesh box/triangle tests (slower)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -190,30 +194,48 @@ def main():
     rend = capi.Renderer(text, device=dev_idx)
     sh = dist_frame.plan_shard(nx, ny, spp, cfg["max_depth"], rank, world, plan=a.plan, tile=a.tile,
                                batch_paths=a.batch_paths, flags=capi.FLAG_COUNT_VISITS if a.count_visits else 0)
-    ex = dist_frame.FrameExchange(sh, dev, dist if world > 1 else None, host_staged=host_reduce)
+    pipeline = not a.no_pipeline
+    ex = dist_frame.FrameExchange(sh, dev, dist if world > 1 else None, host_staged=host_reduce,
+                                  buffers=2 if pipeline else 1)
 
     frame = [None]
 
-    def step():
-        st = rend.render_device(sh.params, ex.local.data_ptr())
-        frame[0] = ex.finish()  # frame-end exchange (RCCL gather) + assembly on rank 0
-        return st
+    def run_frames(n):
+        """n whole frames; returns their stats.  Pipelined: frame k is enqueued,
+        then frame k-1 is waited for and exchanged (RCCL gather + assembly on rank
+        0) from its own buffer while frame k renders."""
+        stats = []
+        if not pipeline:
+            for _ in range(n):
+                stats.append(rend.render_device(sh.params, ex.local.data_ptr()))
+                frame[0] = ex.finish()  # frame-end exchange (RCCL gather) + assembly on rank 0
+            return stats
+        pend = []
+        for k in range(n):
+            buf = ex.locals[k % 2]
+            pend.append((rend.render_device_async(sh.params, buf.data_ptr()), buf))
+            if len(pend) == 2 or k == n - 1:
+                while pend and (len(pend) == 2 or k == n - 1):
+                    t, b = pend.pop(0)
+                    stats.append(rend.wait(t))
+                    frame[0] = ex.finish(b)
+        return stats
 
     def barrier():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
 
-    for _ in range(a.warmup):
-        step()
+    if a.count_visits:
+        pipeline = False  # counted frames are synchronous (SRR_FLAG_COUNT_VISITS)
+    run_frames(a.warmup)
     barrier()
     t0 = time.perf_counter()
     rays = 0
     trace_ms = 0.0
     launches = 0
     visits = [0, 0, 0]
-    for _ in range(a.steps):
-        st = step()
+    for st in run_frames(a.steps):
         visits = [visits[0] + st["box_tests"], visits[1] + st["tri_tests"], visits[2] + st["stack_overflows"]]
         rays += st["world_rays"]
         trace_ms += st["trace_ms"]
@@ -282,7 +304,8 @@ def main():
                                    (f", one {coll} reduce at frame end" if world > 1 else "")),
                        "nx": nx, "ny": ny, "spp_per_gpu" if a.plan == "samples" else "spp": spp,
                        "frame_spp": sh.total_spp, "world_rays_per_step": int(rays_total / a.steps),
-                       "parallelism": f"{a.plan}{world}", "dist_backend": backend if world > 1 else None},
+                       "parallelism": f"{a.plan}{world}", "dist_backend": backend if world > 1 else None,
+                       "frames_in_flight": 2 if pipeline else 1},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                          "traffic": traffic, "kernel": kernel_name, "B_cfg": round(b_cfg, 1),

@@ -197,6 +197,17 @@ int64_t srr_shard_pixels(const srr_params* p, int32_t* pixel_index);
  * in srr_shard_pixels() order.  Inputs are resident on the device; the call
  * returns after the device work finished. */
 int srr_render_device(srr_renderer* r, const srr_params* p, float* d_mean, srr_stats* stats);
+/* Frame pipelining (no reference counterpart: the reference renders one frame
+ * per run).  Enqueue the same frame as srr_render_device and return at once with
+ * a ticket; the renderer keeps two frames in flight on two streams, so a frame's
+ * persistent blocks start on the CUs the previous frame's last paths free.  Fresh
+ * frames of the path engine only (no CONTINUE, KEEP_PATHS, COUNT_VISITS,
+ * WAVEFRONT: SRR_EINVAL).  d_mean must not be read, and must not be the target
+ * of another frame in flight, before srr_render_wait(ticket) returns; enqueueing
+ * a third frame first finishes the oldest (its stats stay for its wait). */
+int srr_render_device_async(srr_renderer* r, const srr_params* p, float* d_mean, int64_t* ticket);
+/* Wait for an async frame and return its stats (each ticket once). */
+int srr_render_wait(srr_renderer* r, int64_t ticket, srr_stats* stats);
 /* Host convenience (the CRender::Run of Render.h:16-51): the shard's pixels
  * (the whole image when shard_count <= 1) as mean radiance (npix*3, may be NULL)
  * and 8-bit tone-mapped rgb8 (npix*3, Raytracing_n.cpp:850-867, may be NULL). */

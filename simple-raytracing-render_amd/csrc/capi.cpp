@@ -398,6 +398,38 @@ int srr_render_device(srr_renderer* r, const srr_params* p, float* d_mean, srr_s
   return 0;
 }
 
+int srr_render_device_async(srr_renderer* r, const srr_params* p, float* d_mean, int64_t* ticket) {
+  if (!r || !p || !d_mean || !ticket) return fail(SRR_EINVAL, "null argument");
+  if (p->spp < 1 || p->max_depth < 0 || p->max_depth > 64) return fail(SRR_EINVAL, "spp >= 1, 0 <= max_depth <= 64");
+  if (p->sample_begin < 0 || p->sample_begin > INT32_MAX - p->spp)
+    return fail(SRR_EINVAL, "sample_begin must be >= 0 and sample_begin + spp must fit in int32");
+  const int key[5] = {p->nx, p->ny, p->shard_index, p->shard_count, p->tile};
+  const bool held = std::equal(key, key + 5, r->pix_key);
+  int64_t npix = held ? r->pix_n : srr_shard_pixels(p, nullptr);
+  if (npix < 0) return (int)npix;
+  std::vector<int32_t> pix;
+  if (!held) {
+    pix.resize(npix);
+    srr_shard_pixels(p, pix.data());
+  }
+  std::string err;
+  int rc = render_device_async(r, p, held ? nullptr : pix.data(), npix, d_mean, ticket, err);
+  if (rc < 0) return fail(rc, err);
+  if (!held) {
+    std::copy(key, key + 5, r->pix_key);
+    r->pix_n = npix;
+  }
+  return 0;
+}
+
+int srr_render_wait(srr_renderer* r, int64_t ticket, srr_stats* stats) {
+  if (!r) return fail(SRR_EINVAL, "null renderer");
+  std::string err;
+  int rc = render_wait(r, ticket, stats, err);
+  if (rc < 0) return fail(rc, err);
+  return 0;
+}
+
 int srr_render(srr_renderer* r, const srr_params* p, float* mean, unsigned char* rgb8, srr_stats* stats) {
   if (!r || !p) return fail(SRR_EINVAL, "null argument");
   int64_t npix = srr_shard_pixels(p, nullptr);
@@ -432,6 +464,7 @@ int srr_accum_get(srr_renderer* r, float* sums, int64_t* npix, int64_t* samples)
 int srr_accum_set(srr_renderer* r, const float* sums, int64_t npix, int64_t samples) {
   if (!r || !sums || npix <= 0 || samples < 0) return fail(SRR_EINVAL, "bad accumulator state");
   HIPCHK(hipSetDevice(r->device));
+  drain_async(r);  // frames in flight read the pixel list this may reallocate
   if ((size_t)npix > r->pix_cap) {
     r->pix_key[0] = -1;  // the held pixel list goes with the buffer
     (void)hipFree(r->pixels);

@@ -153,6 +153,7 @@ int renderer_create(const Scene& sc, int device, srr_renderer** out, std::string
   RCHK(hipStreamCreateWithFlags(&r->acc_st, hipStreamNonBlocking));
   RCHK(hipEventCreate(&r->ev_beg));
   RCHK(hipEventCreate(&r->ev_end));
+  RCHK(hipEventCreateWithFlags(&r->ev_async_in, hipEventDisableTiming));
   for (int l = 0; l < kMaxLanes; ++l) {
     Lane& L = r->lanes[l];
     RCHK(hipStreamCreateWithFlags(&L.st, hipStreamNonBlocking));
@@ -310,48 +311,63 @@ struct AccCommit {
   }
 };
 
+// The stream, buffers and events of one path-engine frame (renderer.h FrameSlot):
+// created on first use, grown as frames need.
+static int slot_init(FrameSlot& F, hipStream_t shared_st, std::string& err) {
+  if (F.ev_beg) return 0;
+  if (shared_st) {
+    F.st = shared_st;
+  } else {
+    RCHK(hipStreamCreateWithFlags(&F.st, hipStreamNonBlocking));
+    F.own_stream = true;
+  }
+  RCHK(hipEventCreate(&F.ev_beg));
+  RCHK(hipEventCreate(&F.ev_end));
+  RCHK(hipMalloc((void**)&F.ctr, 16 * sizeof(unsigned long long)));
+  RCHK(hipHostMalloc((void**)&F.ctr_host, 16 * sizeof(unsigned long long)));
+  return 0;
+}
+
+void slot_free(FrameSlot& F) {
+  (void)hipFree(F.rec);
+  (void)hipFree(F.gstack);
+  (void)hipFree(F.sample);
+  (void)hipFree(F.ctr);
+  (void)hipFree(F.acc);
+  if (F.ctr_host) (void)hipHostFree(F.ctr_host);
+  for (hipEvent_t e : F.win_ev) (void)hipEventDestroy(e);
+  if (F.ev_beg) (void)hipEventDestroy(F.ev_beg);
+  if (F.ev_end) (void)hipEventDestroy(F.ev_end);
+  if (F.own_stream && F.st) (void)hipStreamDestroy(F.st);
+  F = FrameSlot{};
+}
+
 // Path-resident engine (kernels.hip k_paths): one persistent kernel per window
 // of samples; samples land in a [pixel][sample] buffer that k_accumulate_window
 // sums per pixel in sample order, so the image is bitwise the wavefront engine's.
-static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix, int64_t npix, float* d_mean,
-                        srr_stats* stats, std::string& err) {
+// paths_enqueue puts a whole frame on slot F's stream (sums in `acc`, zeroed by
+// the first window when `zero_pending`); paths_finish waits for it and reads its
+// counters.  The caller has staged the pixel list and the Sobol set.
+static int paths_enqueue(srr_renderer* r, FrameSlot& F, const srr_params* p, bool identity, int64_t npix,
+                         float* acc, bool zero_pending, int64_t acc_total, float* d_mean, bool diagnostics,
+                         std::string& err) {
   const bool keep = (p->flags & SRR_FLAG_KEEP_PATHS) != 0;
-  hipStream_t st = r->acc_st;
-  const auto t_host0 = std::chrono::steady_clock::now();
-  srr_stats s{};
-  // pixels: identity for a whole frame, else the shard list
-  bool identity = r->pix_identity;
-  if (pix) {  // a new pixel list (else the renderer holds this shard's already)
-    identity = p->shard_count <= 1;
-    for (int64_t i = 0; identity && i < npix; i += std::max<int64_t>(1, npix / 64)) identity = pix[i] == i;
-    RCHK(stage_pixels(r, pix, npix, identity));
-  }
-  RCHK(ensure_sobol(r, p->sample_begin + p->spp));
-  if (keep) {
-    size_t need = (size_t)npix * p->spp;
-    if (need > r->keep_cap) {
-      (void)hipFree(r->raw_all);
-      (void)hipFree(r->rays_all);
-      RCHK(hipMalloc((void**)&r->raw_all, need * 3 * sizeof(float)));
-      RCHK(hipMalloc((void**)&r->rays_all, need));
-      r->keep_cap = need;
-    }
-    r->kept_paths = (int64_t)need;
-  }
+  hipStream_t st = F.st;
   // persistent lanes and their bounce records
   if (!r->pw_lanes) r->pw_lanes = paths_lanes_per_device(r->view, r->device);
   const size_t rec_need = (size_t)r->pw_lanes * std::max(1, p->max_depth);
-  if (rec_need > r->pw_rec_cap) {
-    (void)hipFree(r->pw_rec);
-    r->pw_rec = nullptr;
-    RCHK(hipMalloc((void**)&r->pw_rec, rec_need * sizeof(float4)));
-    r->pw_rec_cap = rec_need;
+  if (rec_need > F.rec_cap) {
+    (void)hipFree(F.rec);
+    F.rec = nullptr;
+    F.rec_cap = 0;
+    RCHK(hipMalloc((void**)&F.rec, rec_need * sizeof(float4)));
+    F.rec_cap = rec_need;
   }
   // global extension of the BVH4 traversal stack, for meshes deep enough to need it
   // (SRR_GSTACK=0 disables it: every deeper traversal then re-walks the BVH2)
   const char* gs_env = getenv("SRR_GSTACK");
   const int gst_cap = (r->has_meshes && !(gs_env && !atoi(gs_env))) ? kPathsGlobalStack : 0;
-  if (gst_cap && !r->pw_gstack) RCHK(hipMalloc((void**)&r->pw_gstack, (size_t)gst_cap * r->pw_lanes * sizeof(int2)));
+  if (gst_cap && !F.gstack) RCHK(hipMalloc((void**)&F.gstack, (size_t)gst_cap * r->pw_lanes * sizeof(int2)));
   // sample window: all pixels x W samples, buffer within SRR_WINDOW_MB (default 8192)
   size_t budget = (size_t)8192 << 20;
   if (const char* e = getenv("SRR_WINDOW_MB")) budget = (size_t)std::max(1, atoi(e)) << 20;
@@ -364,41 +380,30 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
     return SRR_EINVAL;
   }
   const size_t win_paths = (size_t)npix * W;
-  if (win_paths > r->pw_sample_cap) {
-    (void)hipFree(r->pw_sample);
-    (void)hipFree(r->pw_raw);
-    (void)hipFree(r->pw_rays);
-    r->pw_sample = r->pw_raw = nullptr;
-    r->pw_rays = nullptr;
-    RCHK(hipMalloc((void**)&r->pw_sample, win_paths * 3 * sizeof(float)));
-    r->pw_sample_cap = win_paths;
+  if (win_paths > F.sample_cap) {
+    (void)hipFree(F.sample);
+    F.sample = nullptr;
+    F.sample_cap = 0;
+    RCHK(hipMalloc((void**)&F.sample, win_paths * 3 * sizeof(float)));
+    F.sample_cap = win_paths;
   }
-  if (!r->pw_ctr) RCHK(hipMalloc((void**)&r->pw_ctr, 16 * sizeof(unsigned long long)));
-  if (!r->pw_ctr_host) RCHK(hipHostMalloc((void**)&r->pw_ctr_host, 16 * sizeof(unsigned long long)));
-  RCHK(hipMemsetAsync(r->pw_ctr, 0, 16 * sizeof(unsigned long long), st));
-  // the sums of a fresh frame are zeroed by the first window's accumulation (init)
-  bool zero_pending = false;
-  {
-    const int rc = begin_accum(r, p, npix, st, err, p->spp > 0 ? &zero_pending : nullptr);
-    if (rc < 0) return rc;
-  }
-  const int64_t acc_total = r->acc_samples + p->spp;
+  RCHK(hipMemsetAsync(F.ctr, 0, 16 * sizeof(unsigned long long), st));
   const bool want_sums = (p->flags & SRR_FLAG_SUMS) != 0;
   // per-window HIP events around k_paths, read once the frame is done (no host
   // round trip between windows)
   const int n_windows = (p->spp + W - 1) / W;
-  while ((int)r->win_ev.size() < 2 * n_windows) {
+  while ((int)F.win_ev.size() < 2 * n_windows) {
     hipEvent_t e;
     RCHK(hipEventCreate(&e));
-    r->win_ev.push_back(e);
+    F.win_ev.push_back(e);
   }
-  AccCommit commit{r};
+  F.n_windows = n_windows;
   const bool all_fam = !r->diffuse_only;
   // diagnostics (SRR_WAVE_TIMES=1): per-wave start / exit times of each k_paths launch
   static const bool want_wave_times = getenv("SRR_WAVE_TIMES") != nullptr;
   unsigned long long* wave_times = nullptr;
   const int n_waves = (r->pw_lanes + 63) / 64;
-  if (want_wave_times) {  // owned by the renderer (freed in ~srr_renderer), so no early return leaks it
+  if (want_wave_times && diagnostics) {  // owned by the renderer (freed in ~srr_renderer), so no early return leaks it
     if (!r->pw_wave_times) RCHK(hipMalloc((void**)&r->pw_wave_times, 4 * (size_t)n_waves * sizeof(unsigned long long)));
     wave_times = r->pw_wave_times;
     RCHK(hipMemsetAsync(wave_times, 0, 4 * (size_t)n_waves * sizeof(unsigned long long), st));
@@ -411,8 +416,7 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
   if (!r->pw_slow) RCHK(hipMalloc((void**)&r->pw_slow, (16 * 65536 + 16) * sizeof(float)));
   RCHK(hipMemsetAsync(r->pw_slow + 16 * 65536, 0, 16 * sizeof(float), st));
 #endif
-  RCHK(hipEventRecord(r->ev_beg, st));
-  double kernel_ms = 0;
+  RCHK(hipEventRecord(F.ev_beg, st));
   for (int s0 = 0; s0 < p->spp; s0 += W) {
     const int Wn = std::min(W, p->spp - s0);
     PathWork w{};
@@ -428,39 +432,39 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
     w.base_seed = p->base_seed;
     w.n_paths = (int64_t)npix * Wn;
     w.max_depth = p->max_depth;
-    w.cursor = r->pw_ctr + 1;
-    w.counters = r->pw_ctr;
-    w.sample = r->pw_sample;
+    w.cursor = F.ctr + 1;
+    w.counters = F.ctr;
+    w.sample = F.sample;
     w.raw = keep ? r->raw_all : nullptr;
     w.rays = keep ? r->rays_all : nullptr;
     w.keep_spp = p->spp;
     w.keep_s0 = s0;
-    w.rec = r->pw_rec;
-    w.err = (int*)(r->pw_ctr + 2);
+    w.rec = F.rec;
+    w.err = (int*)(F.ctr + 2);
     const int64_t bl = paths_block_lanes(r->view);  // whole blocks of the launch's size
     w.lanes = (int)std::min<int64_t>(r->pw_lanes, ((w.n_paths + bl - 1) / bl) * bl);
     w.stack_cap = kPathsLdsStack;  // kernels.hip kStack
     if (const char* e = getenv("SRR_STACK_CAP")) w.stack_cap = std::max(1, std::min(kPathsLdsStack, atoi(e)));
-    w.gstack = gst_cap ? r->pw_gstack : nullptr;
+    w.gstack = gst_cap ? F.gstack : nullptr;
     w.gstack_cap = gst_cap;
     w.wave_times = wave_times;
     w.deep_tries = deep_tries;
     w.dbg = getenv("SRR_PATHS_DBG") ? atoi(getenv("SRR_PATHS_DBG")) : 0;
-    w.slow_rays = r->pw_slow;
-    w.slow_count = r->pw_slow ? (unsigned*)(r->pw_slow + 16 * 65536) : nullptr;
+    w.slow_rays = diagnostics ? r->pw_slow : nullptr;
+    w.slow_count = w.slow_rays ? (unsigned*)(r->pw_slow + 16 * 65536) : nullptr;
     const int wi = s0 / W;
-    if (wi > 0) RCHK(hipMemsetAsync(w.cursor, 0, sizeof(unsigned long long), st));  // window 0: zeroed with pw_ctr
-    RCHK(hipEventRecord(r->win_ev[2 * wi], st));
+    if (wi > 0) RCHK(hipMemsetAsync(w.cursor, 0, sizeof(unsigned long long), st));  // window 0: zeroed with ctr
+    RCHK(hipEventRecord(F.win_ev[2 * wi], st));
     launch_paths(r->view, w, all_fam ? 1 : 0, st);
-    RCHK(hipEventRecord(r->win_ev[2 * wi + 1], st));
+    RCHK(hipEventRecord(F.win_ev[2 * wi + 1], st));
     // the last window also writes the output (k_finish fused): means, or raw sums (SRR_FLAG_SUMS)
     const bool last = s0 + Wn >= p->spp;
-    launch_accumulate_window(r->pw_sample, (int)npix, Wn, r->acc, st, wi == 0 && zero_pending, last ? d_mean : nullptr,
+    launch_accumulate_window(F.sample, (int)npix, Wn, acc, st, wi == 0 && zero_pending, last ? d_mean : nullptr,
                              want_sums ? 0 : (int)acc_total);
     if (wave_times) {  // realtime clock: 100 MHz (10 ns ticks)
-      RCHK(hipEventSynchronize(r->win_ev[2 * wi + 1]));
+      RCHK(hipEventSynchronize(F.win_ev[2 * wi + 1]));
       float ms = 0;
-      RCHK(hipEventElapsedTime(&ms, r->win_ev[2 * wi], r->win_ev[2 * wi + 1]));
+      RCHK(hipEventElapsedTime(&ms, F.win_ev[2 * wi], F.win_ev[2 * wi + 1]));
       std::vector<unsigned long long> wt(4 * (size_t)n_waves);
       RCHK(hipMemcpy(wt.data(), wave_times, wt.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
       std::vector<std::pair<double, int>> ex;
@@ -486,25 +490,32 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
       }
       RCHK(hipMemsetAsync(wave_times, 0, wt.size() * sizeof(unsigned long long), st));
     }
-    s.trace_launches += 1;
   }
   if (n_windows == 0) {  // spp 0: nothing rendered, the output is the sums as they stand
     if (want_sums)
-      RCHK(hipMemcpyAsync(d_mean, r->acc, 3 * (size_t)npix * sizeof(float), hipMemcpyDeviceToDevice, st));
+      RCHK(hipMemcpyAsync(d_mean, acc, 3 * (size_t)npix * sizeof(float), hipMemcpyDeviceToDevice, st));
     else
-      launch_finish(r->acc, d_mean, npix, (int)acc_total, st);
+      launch_finish(acc, d_mean, npix, (int)acc_total, st);
   }
-  RCHK(hipMemcpyAsync(r->pw_ctr_host, r->pw_ctr, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
-  RCHK(hipEventRecord(r->ev_end, st));
-  RCHK(hipStreamSynchronize(st));
+  RCHK(hipMemcpyAsync(F.ctr_host, F.ctr, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+  RCHK(hipEventRecord(F.ev_end, st));
+  F.npix = npix;
+  F.paths = npix * p->spp;
+  return 0;
+}
+
+static int paths_finish(srr_renderer* r, FrameSlot& F, const srr_params* p, srr_stats* stats, std::string& err) {
+  RCHK(hipStreamSynchronize(F.st));
   RCHK(hipGetLastError());
-  for (int wi = 0; wi < n_windows; ++wi) {
+  srr_stats s{};
+  double kernel_ms = 0;
+  for (int wi = 0; wi < F.n_windows; ++wi) {
     float ms = 0;
-    RCHK(hipEventElapsedTime(&ms, r->win_ev[2 * wi], r->win_ev[2 * wi + 1]));
+    RCHK(hipEventElapsedTime(&ms, F.win_ev[2 * wi], F.win_ev[2 * wi + 1]));
     kernel_ms += ms;
   }
   unsigned long long ctr[16];
-  std::memcpy(ctr, r->pw_ctr_host, sizeof(ctr));
+  std::memcpy(ctr, F.ctr_host, sizeof(ctr));
   if (getenv("SRR_PATHS_TIMING") && ctr[9]) {
     const double it = (double)ctr[9];
     fprintf(stderr, "k_paths per wave-iteration (ticks): refill %.0f  world %.0f  mesh %.0f  record %.0f  scatter %.0f  fold %.0f  (%llu wave-iterations)\n",
@@ -512,7 +523,7 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
     fprintf(stderr, "  scatter: mixture loop %.0f ticks, %.2f rounds per wave-iteration\n", ctr[13] / it, ctr[14] / it);
   }
 #ifdef SRR_SLOW_RAYS
-  {  // diagnostics build: dump the slow world hits' records (one line per lane, JSON)
+  if (r->pw_slow) {  // diagnostics build: dump the slow world hits' records (one line per lane, JSON)
     unsigned n = 0;
     RCHK(hipMemcpy(&n, r->pw_slow + 16 * 65536, sizeof(unsigned), hipMemcpyDeviceToHost));
     n = std::min(n, 65536u);
@@ -527,26 +538,164 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
               I(b + 9), I(b + 10), I(b + 11), I(b + 12), v[b + 13], I(b + 14), I(b + 15), p->spp);
     }
   }
+#else
+  (void)r;
+  (void)p;
 #endif
-  const unsigned long long rays = ctr[0];
   if (ctr[2]) {
     err = "k_paths index guard tripped (bits " + std::to_string(ctr[2]) + ")";
     return SRR_EIO;
   }
-  r->acc_samples = acc_total;
-  commit.ok = true;
   float total = 0;
-  RCHK(hipEventElapsedTime(&total, r->ev_beg, r->ev_end));
-  s.world_rays = (int64_t)rays;
+  RCHK(hipEventElapsedTime(&total, F.ev_beg, F.ev_end));
+  s.world_rays = (int64_t)ctr[0];
   s.stack_overflows = (int64_t)ctr[11];
   s.deep_traversals = (int64_t)ctr[12];
   s.mixture_capped = (int64_t)ctr[15];
-  s.paths = npix * p->spp;
+  s.paths = F.paths;
   s.trace_ms = kernel_ms;
   s.total_ms = total;
-  (void)t_host0;
+  s.trace_launches = F.n_windows;
   if (stats) *stats = s;
   return 0;
+}
+
+static void finish_slot(srr_renderer* r, FrameSlot& F) {
+  F.busy = false;
+  srr_params none{};
+  F.rc = paths_finish(r, F, &none, &F.stats, F.err);
+  r->done_tickets.push_back({F.ticket, F.rc, F.stats, F.err});
+}
+
+// Frames in flight read the shard's pixel list and the Sobol set: anything that
+// reallocates them waits for those frames first (their stats stay for srr_render_wait).
+void drain_async(srr_renderer* r) {
+  for (FrameSlot& F : r->async_slots)
+    if (F.busy) finish_slot(r, F);
+}
+
+static int paths_stage(srr_renderer* r, const srr_params* p, const int32_t* pix, int64_t npix, bool& identity,
+                       std::string& err) {
+  identity = r->pix_identity;
+  if (pix != nullptr || p->sample_begin + p->spp > r->sobol_n) drain_async(r);
+  if (pix) {  // a new pixel list (else the renderer holds this shard's already)
+    identity = p->shard_count <= 1;
+    for (int64_t i = 0; identity && i < npix; i += std::max<int64_t>(1, npix / 64)) identity = pix[i] == i;
+    RCHK(stage_pixels(r, pix, npix, identity));
+  }
+  RCHK(ensure_sobol(r, p->sample_begin + p->spp));
+  return 0;
+}
+
+static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix, int64_t npix, float* d_mean,
+                        srr_stats* stats, std::string& err) {
+  const bool keep = (p->flags & SRR_FLAG_KEEP_PATHS) != 0;
+  bool identity = false;
+  {
+    const int rc = paths_stage(r, p, pix, npix, identity, err);
+    if (rc < 0) return rc;
+  }
+  if (keep) {
+    size_t need = (size_t)npix * p->spp;
+    if (need > r->keep_cap) {
+      (void)hipFree(r->raw_all);
+      (void)hipFree(r->rays_all);
+      RCHK(hipMalloc((void**)&r->raw_all, need * 3 * sizeof(float)));
+      RCHK(hipMalloc((void**)&r->rays_all, need));
+      r->keep_cap = need;
+    }
+    r->kept_paths = (int64_t)need;
+  }
+  FrameSlot& F = r->sync_slot;
+  {
+    const int rc = slot_init(F, r->acc_st, err);
+    if (rc < 0) return rc;
+  }
+  // the sums of a fresh frame are zeroed by the first window's accumulation (init)
+  bool zero_pending = false;
+  {
+    const int rc = begin_accum(r, p, npix, F.st, err, p->spp > 0 ? &zero_pending : nullptr);
+    if (rc < 0) return rc;
+  }
+  AccCommit commit{r};
+  const int64_t acc_total = r->acc_samples + p->spp;
+  {
+    const int rc = paths_enqueue(r, F, p, identity, npix, r->acc, zero_pending, acc_total, d_mean, true, err);
+    if (rc < 0) return rc;
+  }
+  {
+    const int rc = paths_finish(r, F, p, stats, err);
+    if (rc < 0) return rc;
+  }
+  r->acc_samples = acc_total;
+  commit.ok = true;
+  return 0;
+}
+
+// srr_render_device_async: a fresh frame (no CONTINUE, KEEP_PATHS, COUNT_VISITS or
+// wavefront engine) on one of the renderer's two frame slots, each with its own
+// stream, sums and buffers, so the next frame's persistent blocks take the CUs
+// the previous frame's drain frees.  Returns at once; srr_render_wait reads it.
+int render_device_async(srr_renderer* r, const srr_params* p, const int32_t* pix, int64_t npix, float* d_mean,
+                        int64_t* ticket, std::string& err) {
+  if (p->flags & (SRR_FLAG_CONTINUE | SRR_FLAG_KEEP_PATHS | SRR_FLAG_COUNT_VISITS | SRR_FLAG_WAVEFRONT)) {
+    err = "srr_render_device_async: fresh path-engine frames only (no CONTINUE, KEEP_PATHS, COUNT_VISITS, WAVEFRONT)";
+    return SRR_EINVAL;
+  }
+  if (const char* e = getenv("SRR_ENGINE"); e && !strcmp(e, "wave")) {
+    err = "srr_render_device_async: SRR_ENGINE=wave is synchronous only";
+    return SRR_EINVAL;
+  }
+  RCHK(hipSetDevice(r->device));
+  FrameSlot& F = r->async_slots[r->next_ticket % 2];
+  if (F.busy) finish_slot(r, F);  // the slot's previous frame has not been waited for: finish it now
+  bool identity = false;
+  {
+    const int rc = paths_stage(r, p, pix, npix, identity, err);
+    if (rc < 0) return rc;
+  }
+  {
+    const int rc = slot_init(F, nullptr, err);
+    if (rc < 0) return rc;
+  }
+  if ((size_t)npix > F.acc_cap) {
+    (void)hipFree(F.acc);
+    F.acc = nullptr;
+    F.acc_cap = 0;
+    RCHK(hipMalloc((void**)&F.acc, 3 * (size_t)npix * sizeof(float)));
+    F.acc_cap = npix;
+  }
+  // the caller's stream order: the frame starts after what the legacy stream holds
+  RCHK(hipEventRecord(r->ev_async_in, nullptr));
+  RCHK(hipStreamWaitEvent(F.st, r->ev_async_in, 0));
+  {
+    const int rc = paths_enqueue(r, F, p, identity, npix, F.acc, true, p->spp, d_mean, false, err);
+    if (rc < 0) return rc;
+  }
+  F.ticket = r->next_ticket++;
+  F.busy = true;
+  *ticket = F.ticket;
+  return 0;
+}
+
+int render_wait(srr_renderer* r, int64_t ticket, srr_stats* stats, std::string& err) {
+  RCHK(hipSetDevice(r->device));
+  for (size_t k = 0; k < r->done_tickets.size(); ++k)
+    if (r->done_tickets[k].ticket == ticket) {
+      const DoneTicket d = r->done_tickets[k];
+      r->done_tickets.erase(r->done_tickets.begin() + k);
+      if (stats) *stats = d.stats;
+      err = d.err;
+      return d.rc;
+    }
+  for (FrameSlot& F : r->async_slots)
+    if (F.busy && F.ticket == ticket) {
+      F.busy = false;
+      srr_params none{};
+      return paths_finish(r, F, &none, stats, err);
+    }
+  err = "srr_render_wait: unknown or already waited ticket " + std::to_string(ticket);
+  return SRR_EINVAL;
 }
 
 int render_device(srr_renderer* r, const srr_params* p, const int32_t* pix, int64_t npix, float* d_mean,
@@ -563,6 +712,7 @@ int render_device(srr_renderer* r, const srr_params* p, const int32_t* pix, int6
   // (kernels.hip kWorldLdsBytes) and reads them from global memory otherwise
   if (!wave_engine && !(p->flags & SRR_FLAG_COUNT_VISITS))
     return render_paths(r, p, pix, npix, d_mean, stats, err);
+  drain_async(r);  // the wavefront engine restages the pixel list
   const bool keep = (p->flags & SRR_FLAG_KEEP_PATHS) != 0;
   const int R = kRegionsPerLane;
   hipStream_t ast = r->acc_st;
@@ -801,14 +951,9 @@ srr_renderer::~srr_renderer() {
   (void)hipDeviceSynchronize();
   for (void* p : scene_bufs) (void)hipFree(p);
   if (visits) (void)hipFree(visits);
-  (void)hipFree(pw_rec);
-  (void)hipFree(pw_gstack);
-  (void)hipFree(pw_sample);
-  (void)hipFree(pw_raw);
-  (void)hipFree(pw_rays);
-  (void)hipFree(pw_ctr);
-  if (pw_ctr_host) (void)hipHostFree(pw_ctr_host);
-  for (hipEvent_t e : win_ev) (void)hipEventDestroy(e);
+  srr::slot_free(sync_slot);
+  for (auto& F : async_slots) srr::slot_free(F);
+  if (ev_async_in) (void)hipEventDestroy(ev_async_in);
   (void)hipFree(pw_wave_times);
   (void)hipFree(pw_slow);
   for (auto& L : lanes) {

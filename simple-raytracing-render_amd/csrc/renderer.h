@@ -46,6 +46,40 @@ struct Lane {
   double trace_ms = 0, shade_ms = 0;
 };
 
+// One frame of the path engine: its stream, bounce records, traversal-stack
+// extension, sample window, counters and events (renderer.cpp paths_enqueue);
+// the synchronous path owns one, srr_render_device_async alternates two.
+struct FrameSlot {
+  hipStream_t st = nullptr;
+  bool own_stream = false;
+  hipEvent_t ev_beg = nullptr, ev_end = nullptr;
+  std::vector<hipEvent_t> win_ev;  // per sample window: k_paths start / end
+  float4* rec = nullptr;
+  size_t rec_cap = 0;
+  int2* gstack = nullptr;  // [kPathsGlobalStack][pw_lanes] (kernels.h)
+  float* sample = nullptr;
+  size_t sample_cap = 0;
+  unsigned long long* ctr = nullptr;       // [0] world rays, [1] path cursor, ...
+  unsigned long long* ctr_host = nullptr;  // pinned mirror, read after the frame's stream sync
+  float* acc = nullptr;                    // async slots: the frame's own per-pixel sums
+  size_t acc_cap = 0;
+  // a frame in flight (async slots)
+  bool busy = false;
+  int64_t ticket = -1, npix = 0, paths = 0;
+  int n_windows = 0;
+  int rc = 0;
+  srr_stats stats{};
+  std::string err;
+};
+void slot_free(FrameSlot& F);
+
+struct DoneTicket {  // an async frame finished before its srr_render_wait
+  int64_t ticket;
+  int rc;
+  srr_stats stats;
+  std::string err;
+};
+
 }  // namespace srr
 
 struct srr_renderer {
@@ -67,18 +101,13 @@ struct srr_renderer {
   // path-resident engine (render_paths)
   int pw_lanes = 0;
   bool diffuse_only = false;  // no beckmann / specular materials: lean kernel variant
-  float4* pw_rec = nullptr;
-  size_t pw_rec_cap = 0;
-  int2* pw_gstack = nullptr;  // [kPathsGlobalStack][pw_lanes] (kernels.h)
   bool has_meshes = false;
-  float* pw_sample = nullptr;
-  float* pw_raw = nullptr;
-  uint8_t* pw_rays = nullptr;
-  size_t pw_sample_cap = 0;
-  unsigned long long* pw_ctr = nullptr;  // [0] world rays, [1] path cursor
+  srr::FrameSlot sync_slot;         // srr_render_device (stream acc_st, sums in acc)
+  srr::FrameSlot async_slots[2];    // srr_render_device_async, alternating
+  int64_t next_ticket = 0;
+  std::vector<srr::DoneTicket> done_tickets;
+  hipEvent_t ev_async_in = nullptr;  // orders an async frame after the caller's legacy-stream work
   unsigned long long* pw_wave_times = nullptr;  // SRR_WAVE_TIMES diagnostics, 4 words per wave
-  unsigned long long* pw_ctr_host = nullptr;    // pinned mirror of pw_ctr, read after the frame's stream sync
-  std::vector<hipEvent_t> win_ev;               // per sample window: k_paths start / end
   float* pw_slow = nullptr;  // diagnostics build (-DSRR_SLOW_RAYS): slow world-hit records + count
   int32_t* pixels = nullptr;
   size_t pix_cap = 0;
@@ -104,4 +133,8 @@ int renderer_create(const Scene& s, int device, srr_renderer** out, std::string&
 // them (srr_renderer::pix_key)
 int render_device(srr_renderer* r, const srr_params* p, const int32_t* pix, int64_t npix, float* d_mean,
                   srr_stats* stats, std::string& err);
+int render_device_async(srr_renderer* r, const srr_params* p, const int32_t* pix, int64_t npix, float* d_mean,
+                        int64_t* ticket, std::string& err);
+int render_wait(srr_renderer* r, int64_t ticket, srr_stats* stats, std::string& err);
+void drain_async(srr_renderer* r);  // finish every async frame in flight (results kept for render_wait)
 }  // namespace srr

@@ -59,6 +59,8 @@ def lib():
         L.srr_shard_pixels.restype = ctypes.c_int64
         L.srr_shard_pixels.argtypes = [ctypes.POINTER(Params), vp]
         L.srr_render_device.argtypes = [vp, ctypes.POINTER(Params), vp, ctypes.POINTER(Stats)]
+        L.srr_render_device_async.argtypes = [vp, ctypes.POINTER(Params), vp, ctypes.POINTER(ctypes.c_int64)]
+        L.srr_render_wait.argtypes = [vp, ctypes.c_int64, ctypes.POINTER(Stats)]
         L.srr_merl_load.argtypes = [cp, ip, ctypes.POINTER(vp)]
         L.srr_merl_create.argtypes = [vp, ctypes.c_int64, ip, ctypes.POINTER(vp)]
         L.srr_merl_destroy.argtypes = [vp]
@@ -200,6 +202,20 @@ class Renderer:
         """Render into a device buffer (e.g. a torch tensor's data_ptr())."""
         st = Stats()
         _check(lib().srr_render_device(self.h, ctypes.byref(params), ctypes.c_void_p(d_mean_ptr), ctypes.byref(st)))
+        return st.as_dict()
+
+    def render_device_async(self, params: Params, d_mean_ptr: int) -> int:
+        """Enqueue a fresh frame (srr_render_device_async); returns its ticket.
+        d_mean is written when wait(ticket) returns."""
+        t = ctypes.c_int64()
+        _check(lib().srr_render_device_async(self.h, ctypes.byref(params), ctypes.c_void_p(d_mean_ptr),
+                                             ctypes.byref(t)))
+        return t.value
+
+    def wait(self, ticket: int) -> dict:
+        """Wait for an async frame (srr_render_wait); returns its stats."""
+        st = Stats()
+        _check(lib().srr_render_wait(self.h, ctypes.c_int64(ticket), ctypes.byref(st)))
         return st.as_dict()
 
 

@@ -79,13 +79,16 @@ class FrameExchange:
     or reduce of device tensors), so several ranks may share one GPU; the
     assembled frame is the same bits as over RCCL."""
 
-    def __init__(self, sh: Shard, device, dist=None, host_staged=False):
+    def __init__(self, sh: Shard, device, dist=None, host_staged=False, buffers=1):
         import torch
         self.sh, self.dist, self.torch = sh, dist, torch
         self.host_staged = bool(host_staged and dist is not None)
         nx, ny = sh.params.nx, sh.params.ny
         self.n_max = max(sh.counts)
-        self.local = torch.zeros((self.n_max, 3), dtype=torch.float32, device=device)
+        # `buffers` local outputs: two let frame k+1 render (srr_render_device_async)
+        # while frame k is exchanged from the other
+        self.locals = [torch.zeros((self.n_max, 3), dtype=torch.float32, device=device) for _ in range(buffers)]
+        self.local = self.locals[0]
         self.image = torch.zeros((nx * ny, 3), dtype=torch.float32, device=device)
         xdev = "cpu" if self.host_staged else device  # where the collective's buffers live
         self.xlocal = torch.zeros((self.n_max, 3), dtype=torch.float32, device=xdev) if self.host_staged else None
@@ -97,17 +100,18 @@ class FrameExchange:
         # the renderer's mean: sum * (float)(1.0 / (float)ns)  (kernels.hip k_finish)
         self.inv_ns = torch.tensor(np.float32(1.0 / float(np.float32(sh.total_spp))), device=device)
 
-    def finish(self):
+    def finish(self, local=None):
         sh, torch = self.sh, self.torch
+        local = self.local if local is None else local
         if sh.plan == "tiles":
             if sh.world == 1:
-                self.image[self.idx[0]] = self.local[:sh.counts[0]]
+                self.image[self.idx[0]] = local[:sh.counts[0]]
                 return self.image
             if self.host_staged:
-                self.xlocal.copy_(self.local)
+                self.xlocal.copy_(local)
                 self.dist.gather(self.xlocal, self.gathered, dst=0)
             else:
-                self.dist.gather(self.local, self.gathered, dst=0)  # one exchange over RCCL / xGMI
+                self.dist.gather(local, self.gathered, dst=0)  # one exchange over RCCL / xGMI
             if sh.rank != 0:
                 return None
             for k in range(sh.world):
@@ -116,13 +120,13 @@ class FrameExchange:
         # samples: raw per-pixel sums of this rank's samples, reduced to rank 0
         if sh.world > 1:
             if self.host_staged:
-                self.xlocal.copy_(self.local)
+                self.xlocal.copy_(local)
                 self.dist.reduce(self.xlocal, dst=0)
                 if sh.rank == 0:
-                    self.local.copy_(self.xlocal)
+                    local.copy_(self.xlocal)
             else:
-                self.dist.reduce(self.local, dst=0)
+                self.dist.reduce(local, dst=0)
             if sh.rank != 0:
                 return None
-        torch.mul(self.local, self.inv_ns, out=self.image)
+        torch.mul(local, self.inv_ns, out=self.image)
         return self.image
