@@ -349,9 +349,6 @@ constexpr bool LEAFQ = SRR_LEAFQ != 0;  // mesh_hit4's leaf-triangle queue (A/B:
 #ifndef SRR_TRIPF
 #define SRR_TRIPF 1
 #endif
-#ifndef SRR_NODEPF
-#define SRR_NODEPF 0  // mesh_hit4: touch the next pop's node line ahead (A/B)
-#endif
 
 template <bool PRUNE, bool TIMING = false, bool Q = false, int STRIDE = kTraceBlock>
 SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmin, float tmax, bool is_medium,
@@ -383,9 +380,6 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
   bool overflow = false, deep = false;
   uint32_t nbox = 0, ntri = 0;
   const uint64_t tm_enter = TIMING ? __builtin_amdgcn_s_memtime() : 0;
-#if SRR_NODEPF
-  float pf = 0.f;
-#endif
   for (;;) {
     float4 LX, LY, LZ, HX, HY, HZ;
     int4 CH;
@@ -568,14 +562,6 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
 #undef SRR_CSWAP
     if (kn[0] >= 0) {
       node = kn[0];
-#if SRR_NODEPF
-      // touch the line of the nearest pushed sibling (the next pop) while the
-      // nearest child's subtree is walked: for meshes beyond L2 its fetch is then
-      // an L2 hit (the loaded word itself is never used)
-      if constexpr (!Q) {
-        if (kn[1] >= cx.lds_count) pf = S.node4[8 * (size_t)kn[1]].x;
-      }
-#endif
 #pragma unroll
       for (int c = 3; c >= 1; --c) {
         if (kn[c] < 0) continue;
@@ -612,9 +598,6 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
     if (nx < 0) break;
     node = nx;
   }
-#if SRR_NODEPF
-  asm volatile("" ::"v"(pf));  // keeps the touches (their data is never read)
-#endif
   if (cx.ctr && !TIMING) {
     atomicAdd(cx.ctr, (unsigned long long)nbox);
     atomicAdd(cx.ctr + 1, (unsigned long long)ntri);
