@@ -207,6 +207,26 @@ SRR_D T wload(const T* p, int i) {
   if constexpr ((TR & TR_WL) != 0) return p[i];
   else return cload(p, i);
 }
+// World-list tables are read at wave-uniform addresses (every active lane is at
+// the same object), but the compiler cannot know the loaded words are uniform:
+// uni() moves them to scalar registers, so the dispatch on object / transform
+// kinds becomes scalar branches instead of exec-mask regions (SRR_UNIFORM)
+#ifndef SRR_UNIFORM
+#define SRR_UNIFORM 1
+#endif
+template <class T>
+SRR_D T uni(T v) {
+  static_assert(sizeof(T) % 4 == 0, "uni: whole words");
+  int* w = (int*)&v;
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 4); ++i) w[i] = __builtin_amdgcn_readfirstlane(w[i]);
+  return v;
+}
+template <bool U, class T>
+SRR_D T maybe_uni(T v) {
+  if constexpr (U) return uni(v);
+  else return v;
+}
 constexpr int kTraceBlock = 256;
 constexpr int kStack = kPathsLdsStack;  // LDS stack entries per ray; deeper -> global extension, then the exact BVH2 re-walk
 constexpr int kWorldLdsBytes = kPathsWorldLdsBytes;  // world tables staged in LDS up to this size
@@ -871,11 +891,11 @@ SRR_D bool mesh_hit4_quad(const SceneView& S, const DMesh& m, const Ray& r, floa
 
 // Instance chain (outermost first): the ray going in (hitable.h:44-52, 109-116,
 // 180-188; flip leaves the ray alone)
-template <int TR = 0>
+template <int TR = 0, bool U = false>
 SRR_D Ray chain_in(const SceneView& S, const DObj& ob, Ray r) {
   const int n = ob.xf_count & kXfCountMask;
   for (int k = 0; k < n; ++k) {
-    DXform x = wload<TR>(S.xforms, ob.xf_begin + k);
+    DXform x = maybe_uni<U>(wload<TR>(S.xforms, ob.xf_begin + k));
     if (x.kind == XF_TRANSLATE) r.o = r.o - v3(x.a, x.b, x.c);
     else if (x.kind == XF_ROTY || x.kind == XF_ROTX) {
       int ia = x.kind == XF_ROTY ? 0 : 1;
@@ -919,19 +939,19 @@ struct ObjHit {
 
 // hit of one analytic primitive (sphere, moving sphere, rect, standalone
 // triangle) in its local frame
-template <int TR>
+template <int TR, bool U = false>
 SRR_D bool prim_hit(const SceneView& S, const DObj& ob, const Ray& lr, float tmin, float tmax, bool is_medium,
                     float& t) {
   switch (ob.kind) {
     case OBJ_SPHERE:
     case OBJ_MSPHERE:
-      return sphere_hit(wload<TR>(S.spheres, ob.idx), ob.kind == OBJ_MSPHERE, lr, tmin, tmax, t);
+      return sphere_hit(maybe_uni<U>(wload<TR>(S.spheres, ob.idx)), ob.kind == OBJ_MSPHERE, lr, tmin, tmax, t);
     case OBJ_RECT: {
       float u, v;
-      return rect_hit(wload<TR>(S.rects, ob.idx), lr, tmin, tmax, t, u, v);
+      return rect_hit(maybe_uni<U>(wload<TR>(S.rects, ob.idx)), lr, tmin, tmax, t, u, v);
     }
     case OBJ_TRI: {
-      const DStandaloneTri T = wload<TR>(S.stris, ob.idx);
+      const DStandaloneTri T = maybe_uni<U>(wload<TR>(S.stris, ob.idx));
       V3 p0 = v3(T.p[0], T.p[1], T.p[2]), p1 = v3(T.p[3], T.p[4], T.p[5]), p2 = v3(T.p[6], T.p[7], T.p[8]);
       V3 dir = lr.d / length(lr.d);
       float u, v;
@@ -990,7 +1010,7 @@ SRR_D bool obvh_hit(const SceneView& S, const DObvh& o, const Ray& r, float tmin
 }
 
 // hit of one non-medium flattened object (in its local frame)
-template <int TR>
+template <int TR, bool U = false>
 SRR_D bool basic_hit(const SceneView& S, const DObj& ob, const Ray& lr, float tmin, float tmax, bool is_medium,
                      ObjHit& h, const TraceCtx& cx) {
   switch (ob.kind) {
@@ -999,7 +1019,7 @@ SRR_D bool basic_hit(const SceneView& S, const DObj& ob, const Ray& lr, float tm
       return false;
 #endif
       MeshHit mh;
-      const DMesh m = wload<TR>(S.meshes, ob.idx);
+      const DMesh m = maybe_uni<U>(wload<TR>(S.meshes, ob.idx));
       bool hit;
       if (tr_mode(TR) == TR_BVH2) hit = mesh_hit<false>(S, m, lr, tmin, tmax, is_medium, mh, cx.ctr);
       else if (TR & TR_QUAD)
@@ -1019,7 +1039,7 @@ SRR_D bool basic_hit(const SceneView& S, const DObj& ob, const Ray& lr, float tm
     case OBJ_MEDIUM:
       return false;
     default:
-      return prim_hit<TR>(S, ob, lr, tmin, tmax, is_medium, h.t);
+      return prim_hit<TR, U>(S, ob, lr, tmin, tmax, is_medium, h.t);
   }
 }
 
@@ -1031,8 +1051,8 @@ SRR_D bool list_hit(const SceneView& S, int b, int n, const Ray& r, float tmin, 
   bool any = false;
   float closest = tmax;
   for (int k = 0; k < n; ++k) {
-    const DObj ob = wload<TR>(S.objs, b + k);
-    const Ray lr = chain_in<TR>(S, ob, r);
+    const DObj ob = maybe_uni<SRR_UNIFORM != 0>(wload<TR>(S.objs, b + k));
+    const Ray lr = chain_in<TR, SRR_UNIFORM != 0>(S, ob, r);
     float th = 0;
     bool hit;
     if (ob.kind == OBJ_MESH) {
@@ -1049,7 +1069,7 @@ SRR_D bool list_hit(const SceneView& S, int b, int n, const Ray& r, float tmin, 
     } else if (ob.kind == OBJ_MEDIUM) {
       hit = false;
     } else {
-      hit = prim_hit<TR>(S, ob, lr, tmin, closest, true, th);
+      hit = prim_hit<TR, SRR_UNIFORM != 0>(S, ob, lr, tmin, closest, true, th);
     }
     if (hit) {
       any = true;
@@ -1105,15 +1125,15 @@ SRR_D void world_objs(const SceneView& S, const Ray& r, Rng& rng, const TraceCtx
                       float& closest) {
   const float tmin = 0.001f;
   for (int k = k0; k < k1; ++k) {
-    const DObj ob = wload<TR>(S.objs, k);
-    Ray lr = chain_in<TR>(S, ob, r);
+    const DObj ob = maybe_uni<SRR_UNIFORM != 0>(wload<TR>(S.objs, k));
+    Ray lr = chain_in<TR, SRR_UNIFORM != 0>(S, ob, r);
     ObjHit h;
     bool hit;
     if (MEDIA && ob.kind == OBJ_MEDIUM) {
-      hit = medium_hit<TR>(S, wload<TR>(S.media, ob.idx), lr, tmin, closest, rng, h.t, cx);
+      hit = medium_hit<TR>(S, maybe_uni<SRR_UNIFORM != 0>(wload<TR>(S.media, ob.idx)), lr, tmin, closest, rng, h.t, cx);
       h.prim = -1;
     } else {
-      hit = basic_hit<TR>(S, ob, lr, tmin, closest, false, h, cx);
+      hit = basic_hit<TR, SRR_UNIFORM != 0>(S, ob, lr, tmin, closest, false, h, cx);
     }
     if (hit) {
       closest = h.t;
@@ -1130,15 +1150,15 @@ SRR_D WorldHit world_hit(const SceneView& S, const Ray& r, Rng& rng, const Trace
   float closest = FLT_MAX;  // numeric_limits<float>::max(), Raytracing_n.cpp:58
   const float tmin = 0.001f;
   for (int k = 0; k < S.n_world; ++k) {
-    const DObj ob = wload<TR>(S.objs, k);
-    Ray lr = chain_in<TR>(S, ob, r);
+    const DObj ob = maybe_uni<SRR_UNIFORM != 0>(wload<TR>(S.objs, k));
+    Ray lr = chain_in<TR, SRR_UNIFORM != 0>(S, ob, r);
     ObjHit h;
     bool hit;
     if (MEDIA && ob.kind == OBJ_MEDIUM) {
-      hit = medium_hit<TR>(S, wload<TR>(S.media, ob.idx), lr, tmin, closest, rng, h.t, cx);
+      hit = medium_hit<TR>(S, maybe_uni<SRR_UNIFORM != 0>(wload<TR>(S.media, ob.idx)), lr, tmin, closest, rng, h.t, cx);
       h.prim = -1;
     } else {
-      hit = basic_hit<TR>(S, ob, lr, tmin, closest, false, h, cx);
+      hit = basic_hit<TR, SRR_UNIFORM != 0>(S, ob, lr, tmin, closest, false, h, cx);
     }
     if (hit) {
       closest = h.t;
