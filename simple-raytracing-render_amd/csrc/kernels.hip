@@ -2496,7 +2496,8 @@ constexpr int kPathsLdsNodesCmp = 56;  // LDS node cache of the CMP variant (roo
 // BS: lanes per block.  256 (4 blocks per CU) or 1,024 (one block per CU, the same
 // 4 waves per SIMD): one LDS allocation per CU, whose 160 KB then cache
 // kPathsLdsNodesBig BVH4 nodes (the top ~5 levels) instead of 96.
-constexpr int kPathsLdsNodesBig = 696;  // 8 KB world + 64 KB stacks + 696 x 128 B < 160 KB
+// 8 KB world + 8 B x kStack x 1,024 lanes of stacks + the node cache <= 160 KB (696 nodes at kStack 8)
+constexpr int kPathsLdsNodesBig = (160 * 1024 - 8192 - 8 * kPathsLdsStack * 1024 - 1024) / 128;
 
 template <bool MEDIA, bool ALLFAM, int MINB, bool TIMED = false, bool WL = true, bool QUAD = false, bool CMP = false,
           bool CQ = false, int BS = kPathsBlock>
