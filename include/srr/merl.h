@@ -2,7 +2,10 @@
 // table index of an (in, out) direction pair in half/difference-angle
 // coordinates (Rusinkiewicz), and the scaled RGB value stored there.  Host and
 // device share this code; every operation is double precision in the
-// reference's order (kernels are built with -ffp-contract=off).
+// reference's order (kernels are built with -ffp-contract=off), and the
+// reference's double cos / sin / acos / atan2 are glibc's own algorithms
+// (glibc_math64.h), so the cell of every query -- out == in included, where
+// phi_diff is atan2 of ~1e-17 residues -- is the reference's.
 //
 // Reference: brdf.h:7-15 (resolution, channel scales), :17-61 (index
 // functions), :70-154 (vector helpers, std_coords_to_half_diff_coords),
@@ -13,8 +16,10 @@
 #include <cmath>
 #include <cstdint>
 
+#include "glibc_math64.h"
+
 #if defined(__HIPCC__)
-#define SRR_HD __host__ __device__ inline
+#define SRR_HD __device__ inline  // (glibc_math64.h's tables live in device memory)
 #else
 #define SRR_HD inline
 #endif
@@ -59,7 +64,7 @@ SRR_HD void unit3(double* v) {  // brdf::normalize
 // Rodrigues rotation of v about a unit axis (brdf::rotate_vector), summed in the
 // reference's order: v cos, + axis (axis.v)(1 - cos), + (axis x v) sin
 SRR_HD void rotate(const double* v, const double* axis, double angle, double* out) {
-  const double c = cos(angle), s = sin(angle);
+  const double c = gm64::cos(angle), s = gm64::sin(angle);
   for (int k = 0; k < 3; ++k) out[k] = v[k] * c;
   double d = axis[0] * v[0] + axis[1] * v[1] + axis[2] * v[2];
   d = d * (1.0 - c);
@@ -74,24 +79,31 @@ SRR_HD void rotate(const double* v, const double* axis, double angle, double* ou
 // difference vector from the normalised incoming one.
 SRR_HD void half_diff(double theta_in, double fi_in, double theta_out, double fi_out, double& theta_half,
                       double& fi_half, double& theta_diff, double& fi_diff) {
-  const double iz = cos(theta_in), ip = sin(theta_in);
-  const double ix = ip * cos(fi_in), iy = ip * sin(fi_in);
+  // (the reference's g++ -O2 build merges each of the four angles' sin and cos
+  // into one glibc sincos() call -- a different, non-FMA build of the algorithm --
+  // while rotate()'s cos / sin stay separate calls)
+  double ip, iz, sfi, cfi;
+  gm64::sincos(theta_in, ip, iz);
+  gm64::sincos(fi_in, sfi, cfi);
+  const double ix = ip * cfi, iy = ip * sfi;
   double in[3] = {ix, iy, iz};
   unit3(in);
-  const double oz = cos(theta_out), op = sin(theta_out);
-  const double ox = op * cos(fi_out), oy = op * sin(fi_out);
+  double op, oz, sfo, cfo;
+  gm64::sincos(theta_out, op, oz);
+  gm64::sincos(fi_out, sfo, cfo);
+  const double ox = op * cfo, oy = op * sfo;
   double out[3] = {ox, oy, oz};
   unit3(out);  // (unused afterwards, as in the reference)
   double h[3] = {(ix + ox) / 2.0, (iy + oy) / 2.0, (iz + oz) / 2.0};
   unit3(h);
-  theta_half = acos(h[2]);
-  fi_half = atan2(h[1], h[0]);
+  theta_half = gm64::acos(h[2]);
+  fi_half = gm64::atan2(h[1], h[0]);
   const double binormal[3] = {0.0, 1.0, 0.0}, normal[3] = {0.0, 0.0, 1.0};
   double tmp[3], diff[3];
   rotate(in, normal, -fi_half, tmp);
   rotate(tmp, binormal, -theta_half, diff);
-  theta_diff = acos(diff[2]);
-  fi_diff = atan2(diff[1], diff[0]);
+  theta_diff = gm64::acos(diff[2]);
+  fi_diff = gm64::atan2(diff[1], diff[0]);
 }
 
 // lookup_brdf_val's table cell (brdf.h:199-203): phi_half is ignored (isotropic)

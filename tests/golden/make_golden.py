@@ -42,7 +42,7 @@ RENDERS = [
 
 KATS = [("erf", 512), ("beckmann11", 512), ("beckmann_dist", 512), ("beckmann_pdf", 512), ("cosine_pdf", 256),
         ("orennayar_pdf", 256), ("dielectric", 256), ("metal", 256), ("triangle", 1024), ("aabb", 1024),
-        ("camera", 256), ("lights", 256), ("light_list", 256), ("merl", 2048)]
+        ("camera", 256), ("lights", 256), ("light_list", 256), ("merl", 2048), ("merl_same", 4096)]
 
 
 def run(*args):
