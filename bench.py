@@ -8,9 +8,10 @@
 One step = one whole frame through the C-ABI (srr_render_device, inputs
 resident in HBM) on every rank, then the frame-end exchange over RCCL
 (srr/dist.py).  Default plan "tiles" (strong scaling, the
-north_star split): the BASELINE config's one 512x512x1024 frame, 16x16 tiles
-(--tile) round-robin over the N GPUs (each tile row rotated by one), one gather of the tiles' means to rank 0 (the
-image is bitwise the 1-GPU image).  Plan "samples" (weak scaling): each GPU
+north_star split): the BASELINE config's one 512x512x1024 frame, tiles of edge
+--tile (default 1: single pixels) dealt round-robin over the N GPUs (each tile row
+rotated by one), one gather of the tiles' means to rank 0 (the image is bitwise
+the 1-GPU image).  Plan "samples" (weak scaling): each GPU
 renders 512x512x1024 paths as its sample range of one N*1024-spp frame; one
 reduce of raw per-pixel sums.  A "sample" is one world ray segment (one
 reference world->hit call).  Rank 0 prints one JSON line.
@@ -18,6 +19,7 @@ reference world->hit call).  Rank 0 prints one JSON line.
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -62,6 +64,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--count-visits", action="store_true", help="diagnostic: count mesh box/triangle tests (slower)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--force-dist", action="store_true",
+                    help="take the multi-rank code path even at world size 1 (init_process_group over "
+                         "SRR_DIST_BACKEND, the frame-end gather/reduce through the collective): run under "
+                         "torch.distributed.run --nproc-per-node 1 it executes the RCCL leg on one GPU")
     ap.add_argument("--save-frame", default="",
                     help="rank 0 saves the assembled frame of the last step (per-pixel means, .npy)")
     return ap.parse_args()
@@ -171,14 +177,26 @@ def main():
         raise SystemExit(f"SRR_DIST_BACKEND must be nccl or gloo, not {backend!r}")
     n_dev = torch.cuda.device_count()  # counting devices does not initialise the GPU
     dev_idx = local % max(n_dev, 1)
-    if world > 1:
+    use_dist = world > 1 or a.force_dist
+    if a.force_dist and "MASTER_ADDR" not in os.environ:
+        raise SystemExit("--force-dist: run under torch.distributed.run (MASTER_ADDR/MASTER_PORT unset)")
+    dist_world = 1
+    if use_dist:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
         else:
             dist.init_process_group("gloo")
+        dist_world = dist.get_world_size()
+        if dist_world != world:
+            raise SystemExit(f"communicator has {dist_world} ranks, WORLD_SIZE says {world}")
+    if a.gpus != world:
+        raise SystemExit(f"--gpus {a.gpus} but {world} rank(s) were launched (use torch.distributed.run "
+                         f"--nproc-per-node {a.gpus})")
+    if backend == "nccl" and use_dist and n_dev < world:
+        raise SystemExit(f"RCCL wants one GPU per rank: {world} ranks, {n_dev} GPUs visible")
     torch.cuda.set_device(dev_idx)
     dev = torch.device("cuda", dev_idx)
-    host_reduce = world > 1 and backend == "gloo"
+    host_reduce = use_dist and backend == "gloo"
 
     dv = {"divs": a.divs} if a.divs else {}
     if a.divs and a.scene in ("s1", "s4_real"):
@@ -195,7 +213,7 @@ def main():
     sh = dist_frame.plan_shard(nx, ny, spp, cfg["max_depth"], rank, world, plan=a.plan, tile=a.tile,
                                batch_paths=a.batch_paths, flags=capi.FLAG_COUNT_VISITS if a.count_visits else 0)
     pipeline = not a.no_pipeline
-    ex = dist_frame.FrameExchange(sh, dev, dist if world > 1 else None, host_staged=host_reduce,
+    ex = dist_frame.FrameExchange(sh, dev, dist if use_dist else None, host_staged=host_reduce,
                                   buffers=2 if pipeline else 1)
 
     frame = [None]
@@ -222,7 +240,7 @@ def main():
         return stats
 
     def barrier():
-        if world > 1:
+        if use_dist:
             dist.barrier()
         torch.cuda.synchronize()
 
@@ -244,7 +262,7 @@ def main():
     elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed, float(rays), trace_ms], dtype=torch.float64,
                      device="cpu" if host_reduce else dev)
-    if world > 1:
+    if use_dist:
         tmax = t[:1].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         tsum = t[1:].clone()
@@ -258,6 +276,7 @@ def main():
         np.save(a.save_frame, frame[0].cpu().numpy())
     if rank == 0:
         coll = "RCCL" if backend == "nccl" else "host-staged gloo"
+        launches_total = launches
         counts_json = json.load(open(os.path.join(ROOT, "tests", "golden", "traversal_counts.json")))
         key = CONFIG_KEY[a.scene]
         default_divs = {"s2": 10, "s3": 10, "s3_metal": 10, "s4": 40, "s5": 40}.get(a.scene)
@@ -274,11 +293,18 @@ def main():
         kernel_name = ("k_trace (wavefront engine)" if wave else
                        "k_paths (path-resident persistent kernel: trace + shade)")
         traffic = None
+        # measured HBM bytes of k_paths (tools/pmc_traffic.py).  A summary that records its
+        # frame's world rays is priced per world ray on this run's launches; an older one only
+        # stands for the default single-GPU frame it was measured on
         pmc = os.path.join(ROOT, "profiles", f"pmc_{a.scene}{key[len(CONFIG_KEY[a.scene]):]}.json")
-        if os.path.exists(pmc):
+        default_frame = (world == 1 and a.plan == "tiles" and (nx, ny, spp) == (cfg["nx"], cfg["ny"], cfg["spp"]))
+        if os.path.exists(pmc) and launches:
             pj = json.load(open(pmc))
             if pj.get("kernel", "") in kernel_name:
-                traffic = pj.get("hbm_bytes_per_launch")
+                if pj.get("world_rays_per_launch"):
+                    traffic = round(pj["hbm_bytes_per_launch"] / pj["world_rays_per_launch"] * rays / launches)
+                elif default_frame:
+                    traffic = pj.get("hbm_bytes_per_launch")
         out = {
             "metric": "Msamples/s (rays x bounces) + HBM GB/s vs roofline, Cornell+teapot 1024spp",
             "value": round(value, 3),
@@ -297,44 +323,63 @@ def main():
             "config": {"workload": f"{key}: {a.scene}{f' divs {a.divs}' if a.divs else ''} {nx}x{ny} {spp}spp "
                                    f"maxDepth {cfg['max_depth']}" + (
                                    (f", {a.tile}x{a.tile} tiles round-robin over {world} GPUs, one {coll} gather "
-                                    f"to rank 0 at frame end" if world > 1 else
+                                    f"to rank 0 at frame end" if use_dist else
                                     ", whole frame on one GPU (no collective)")
                                    if a.plan == "tiles" else
                                    f" per GPU; {world} GPU(s) render sample ranges of one {spp * world}spp frame" +
-                                   (f", one {coll} reduce at frame end" if world > 1 else "")),
+                                   (f", one {coll} reduce at frame end" if use_dist else "")),
                        "nx": nx, "ny": ny, "spp_per_gpu" if a.plan == "samples" else "spp": spp,
                        "frame_spp": sh.total_spp, "world_rays_per_step": int(rays_total / a.steps),
-                       "parallelism": f"{a.plan}{world}", "dist_backend": backend if world > 1 else None,
+                       "parallelism": f"{a.plan}{world}", "dist_backend": backend if use_dist else None,
+                       "dist_world": dist_world if use_dist else None, "devices_seen": n_dev,
                        "frames_in_flight": 2 if pipeline else 1},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                          "traffic": traffic, "kernel": kernel_name, "B_cfg": round(b_cfg, 1),
                          "trace_ms_per_launch": round(trace_ms / max(launches, 1), 4),
+                         "trace_launches": launches_total,
                          "basis": "achieved/frac count ALGORITHMIC bytes: B_cfg per world ray from the "
                                   "reference's traversal counts (SURVEY 8(d)); traffic is the measured HBM bytes",
                          "traffic_GBps": (round(traffic / (trace_ms / max(launches, 1) * 1e-3) / 1e9, 1)
                                           if traffic and trace_ms > 0 else None),
-                         "measured_bound": "issue/latency: the scene lives in LDS and L2, measured HBM traffic is a "
-                                           "few % of peak (profiles/r02/counters_*.json)"},
+                         "measured_bound": "issue/latency: the scene lives in LDS and L2 (no counter summary of "
+                                           "this config in profiles/)"},
         }
-        # issue roofline of the same kernel from a committed PMC summary of this build
-        # (tools/counters.sh -> profiles/r03/counters_<scene>.json): VALU wave-instructions
-        # per launch over the live launch time, against 1,024 SIMDs each issuing one
-        # wave64 VALU instruction per 2 cycles (SIMD-32, MI355X_MICROARCH.md)
-        cnt = os.path.join(ROOT, "profiles", "r03", f"counters_{a.scene}{key[len(CONFIG_KEY[a.scene]):]}.json")
-        if os.path.exists(cnt) and trace_ms > 0:
-            cj = json.load(open(cnt))
-            insts = cj["raw_per_launch"]["SQ_INSTS_VALU"]
+        # issue roofline of the same kernel from a committed PMC summary (tools/counters.sh ->
+        # profiles/rNN/counters_<scene>.json, newest round first): VALU wave-instructions per
+        # world ray of the profiled frame, times the world rays rank 0 traced here, over rank 0's
+        # live kernel time -- so a shard, another frame size or another spp is priced by its own
+        # rays, not by the profiled frame's -- against 1,024 SIMDs each issuing one wave64 VALU
+        # instruction per 2 cycles (SIMD-32, MI355X_MICROARCH.md)
+        cj, cnt = None, None
+        suffix = key[len(CONFIG_KEY[a.scene]):]
+        for rdir in sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]")), reverse=True):
+            f = os.path.join(rdir, f"counters_{a.scene}{suffix}.json")
+            if os.path.exists(f):
+                j = json.load(open(f))
+                if j.get("world_rays_per_launch"):
+                    cj, cnt = j, f
+                    break
+        if cj is not None and trace_ms > 0 and rays > 0:
+            insts_per_ray = cj["raw_per_launch"]["SQ_INSTS_VALU"] / cj["world_rays_per_launch"]
             clock = cj.get("clock_ghz") or 2.4
-            rate = insts / (trace_ms / max(launches, 1) * 1e-3)
+            rate = insts_per_ray * rays / (trace_ms * 1e-3)
             peak = 1024 * clock * 1e9 / 2
             lane = cj.get("valu_lane_utilisation")
             out["roofline"]["issue"] = {
                 "valu_wave_insts_per_s": round(rate, -6), "peak": round(peak, -6), "frac": round(rate / peak, 4),
                 "lane_utilisation": lane, "lane_frac": round(rate / peak * lane, 4) if lane else None,
+                "valu_wave_insts_per_world_ray": round(insts_per_ray, 3),
                 "wave_time_split": cj.get("wave_time_split"), "clock_ghz": clock,
-                "source": os.path.relpath(cnt, ROOT) + f" ({cj.get('ms_per_launch_profiled')} ms/launch profiled)"}
+                "source": os.path.relpath(cnt, ROOT) + f" ({cj.get('ms_per_launch_profiled')} ms/launch profiled, "
+                          f"{cj.get('profiled_workload', '?')})"}
             ws = cj.get("wave_time_split") or {}
+            hbm = cj.get("hbm") or {}
+            if traffic is None and hbm.get("total_bytes"):
+                # measured HBM bytes per world ray of the profiled frame, priced on this run's launches
+                traffic = round(hbm["total_bytes"] / cj["world_rays_per_launch"] * rays / max(launches, 1))
+                out["roofline"]["traffic"] = traffic
+                out["roofline"]["traffic_GBps"] = round(traffic / (trace_ms / max(launches, 1) * 1e-3) / 1e9, 1)
             out["roofline"]["measured_bound"] = (
                 f"latency/issue: VALU pipe {100 * rate / peak:.0f}% busy at {100 * (lane or 0):.0f}% lane "
                 f"utilisation, waves {100 * ws.get('waiting_on_memory_or_barrier', 0):.0f}% of their time waiting; "

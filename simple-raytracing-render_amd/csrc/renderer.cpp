@@ -560,6 +560,15 @@ static int paths_finish(srr_renderer* r, FrameSlot& F, const srr_params* p, srr_
   return 0;
 }
 
+// frees a slot's sample window (the largest per-frame buffer); the next frame
+// on the slot allocates it again
+static void release_window(FrameSlot& F) {
+  if (!F.sample) return;
+  (void)hipFree(F.sample);
+  F.sample = nullptr;
+  F.sample_cap = 0;
+}
+
 static void finish_slot(srr_renderer* r, FrameSlot& F) {
   F.busy = false;
   srr_params none{};
@@ -607,6 +616,12 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
     r->kept_paths = (int64_t)need;
   }
   FrameSlot& F = r->sync_slot;
+  // one sample window per mode: synchronous frames release the async slots' windows
+  // (each up to SRR_WINDOW_MB) instead of holding three
+  if (r->async_slots[0].sample || r->async_slots[1].sample) {
+    drain_async(r);
+    for (FrameSlot& A : r->async_slots) release_window(A);
+  }
   {
     const int rc = slot_init(F, r->acc_st, err);
     if (rc < 0) return rc;
@@ -621,7 +636,10 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
   const int64_t acc_total = r->acc_samples + p->spp;
   {
     const int rc = paths_enqueue(r, F, p, identity, npix, r->acc, zero_pending, acc_total, d_mean, true, err);
-    if (rc < 0) return rc;
+    if (rc < 0) {
+      (void)hipStreamSynchronize(F.st);  // windows already enqueued must not outlive the error
+      return rc;
+    }
   }
   {
     const int rc = paths_finish(r, F, p, stats, err);
@@ -649,6 +667,7 @@ int render_device_async(srr_renderer* r, const srr_params* p, const int32_t* pix
   RCHK(hipSetDevice(r->device));
   FrameSlot& F = r->async_slots[r->next_ticket % 2];
   if (F.busy) finish_slot(r, F);  // the slot's previous frame has not been waited for: finish it now
+  release_window(r->sync_slot);   // (idle: synchronous frames return finished)
   bool identity = false;
   {
     const int rc = paths_stage(r, p, pix, npix, identity, err);
@@ -670,7 +689,11 @@ int render_device_async(srr_renderer* r, const srr_params* p, const int32_t* pix
   RCHK(hipStreamWaitEvent(F.st, r->ev_async_in, 0));
   {
     const int rc = paths_enqueue(r, F, p, identity, npix, F.acc, true, p->spp, d_mean, false, err);
-    if (rc < 0) return rc;
+    if (rc < 0) {
+      // windows already on F.st read the slot's buffers: drain them before the slot is reused
+      (void)hipStreamSynchronize(F.st);
+      return rc;
+    }
   }
   F.ticket = r->next_ticket++;
   F.busy = true;

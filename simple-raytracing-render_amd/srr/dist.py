@@ -5,7 +5,8 @@ Every (pixel, sample) path is independent and the scene is read-only, so a
 frame shards with no exchange until the end.  Two plans:
 
 * ``tiles``   (strong scaling, a fixed frame; the default): rank k renders the
-  32x32 tiles t (in tile row tr) with (t + tr) % world == k, all samples: round
+  tiles t of edge ``tile`` (bench.py default 1: single pixels) in tile row tr
+  with (t + tr) % world == k, all samples: round
   robin with each tile row rotated by one, so no rank gets whole tile columns
   (srr_shard_pixels).  Frame end: one gather of
   the packed per-pixel means to rank 0, which scatters them into the image.
@@ -73,7 +74,11 @@ class FrameExchange:
     `local` is this rank's [n_max, 3] float32 tensor of per-pixel means
     (``tiles``; rows beyond its pixel count are ignored) or sample sums
     (``samples``).  `finish()` returns the assembled [nx*ny, 3] frame of means
-    on rank 0 (None elsewhere).
+    on rank 0 (None elsewhere).  With one rank and no communicator, in PPM
+    order, that frame is a VIEW of the buffer it was rendered into: with
+    buffers=2, the frame two steps later overwrites it (copy it to keep it).
+    With a communicator (``dist``) the collective runs even at world size 1
+    (bench.py --force-dist: the RCCL leg on one GPU).
 
     host_staged: the collective runs on host copies (gloo, which has no gather
     or reduce of device tensors), so several ranks may share one GPU; the
@@ -106,7 +111,7 @@ class FrameExchange:
         sh, torch = self.sh, self.torch
         local = self.local if local is None else local
         if sh.plan == "tiles":
-            if sh.world == 1:
+            if self.dist is None:
                 if self.identity:
                     return local[:sh.counts[0]]  # (a view of the buffer the frame was rendered into)
                 self.image[self.idx[0]] = local[:sh.counts[0]]
@@ -122,7 +127,7 @@ class FrameExchange:
                 self.image[self.idx[k]] = self.gathered[k][:sh.counts[k]].to(self.image.device)
             return self.image
         # samples: raw per-pixel sums of this rank's samples, reduced to rank 0
-        if sh.world > 1:
+        if self.dist is not None:
             if self.host_staged:
                 self.xlocal.copy_(local)
                 self.dist.reduce(self.xlocal, dst=0)

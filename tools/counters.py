@@ -57,6 +57,16 @@ def main():
         rd, wr = g("FETCH_SIZE") * 1024 * 2, g("WRITE_SIZE") * 1024
         out["hbm"] = {"read_bytes": round(rd), "write_bytes": round(wr), "total_bytes": round(rd + wr),
                       "GBps_at_profiled_time": round((rd + wr) / (ms * 1e-3) / 1e9, 1) if ms else None}
+    # the profiled frame (bench.py's JSON line of the first pass): bench.py prices
+    # these per-launch counts per world ray on whatever frame it runs
+    for log in sorted(glob.glob(prefix + ".p*.log")):
+        lines = [l for l in open(log, errors="replace") if l.startswith("{")]
+        if lines:
+            b = json.loads(lines[-1])
+            launches = b["roofline"].get("trace_launches") or 1
+            out["world_rays_per_launch"] = round(b["config"]["world_rays_per_step"] * b["steps"] / launches)
+            out["profiled_workload"] = b["config"]["workload"]
+            break
     print(json.dumps(out, indent=1))
 
 

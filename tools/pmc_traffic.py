@@ -1,7 +1,10 @@
 """Reduce rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes to HBM bytes per launch
 of one kernel, written as the JSON bench.py reads for roofline.traffic.
 
-usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR KERNEL_SUBSTR OUT.json
+usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR KERNEL_SUBSTR OUT.json [BENCH_LOG]
+
+BENCH_LOG (bench.py's output of the profiled run) adds the frame's world rays
+per launch, so bench.py can price the bytes per world ray on any frame.
 
 Corrections (MI355X_MICROARCH.md, HBM/rocprofv3 section): FETCH_SIZE and
 WRITE_SIZE are reported in KiB; on gfx950 FETCH_SIZE counts 64 B per 128-B
@@ -42,6 +45,13 @@ def main():
         "hbm_bytes_per_launch": round(read_b + write_b),
         "corrections": "FETCH_SIZE KiB x1024 x2 (gfx950 64B-per-128B-request tally); WRITE_SIZE KiB x1024",
     }
+    if len(sys.argv) > 5:
+        lines = [l for l in open(sys.argv[5], errors="replace") if l.startswith("{")]
+        b = json.loads(lines[-1])
+        launches = b["roofline"].get("trace_launches") or 1
+        res["world_rays_per_launch"] = round(b["config"]["world_rays_per_step"] * b["steps"] / launches)
+        res["hbm_bytes_per_world_ray"] = round(res["hbm_bytes_per_launch"] / res["world_rays_per_launch"], 2)
+        res["profiled_workload"] = b["config"]["workload"]
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
 
