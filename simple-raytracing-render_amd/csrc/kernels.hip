@@ -2493,11 +2493,68 @@ constexpr unsigned long long kPoolChunk = 64;  // path indices a wave takes per 
 // result of every ray is mesh_hit4's, so paths stay bit-identical.
 constexpr int kPathsLdsNodesCmp = 56;  // LDS node cache of the CMP variant (room for the queue)
 
+// Camera-ray ring (SRR_RAYRING, default on).  A lane whose path ended used to
+// generate its next camera ray itself (pixel and sample from the path index,
+// per-path seeds, Sobol point, lens disk, normalisation: a few hundred VALU
+// instructions) while the wave's other lanes, still inside their paths, idled:
+// about half the lanes refill per wave-iteration (C2 paths average 2.03 world
+// rays), so the refill ran at ~50 % lane utilisation every iteration.  With the
+// ring, the wave generates the camera rays of a whole 64-path chunk at once --
+// lane k the ray of path chunk + k, every lane busy -- into its 64 LDS entries,
+// and refilling lanes just read theirs: the chunk's rays cost one full-wave
+// generation per ~2 iterations instead of a half-empty one per iteration.  Every
+// path's ray is the same function of its index, so paths are unchanged.
+#ifndef SRR_RAYRING
+#define SRR_RAYRING 1
+#endif
+constexpr int kRingWords = 11;  // o.xyz, d.xyz, time, lcg (2 words), pcg (2 words)
+
 // BS: lanes per block.  256 (4 blocks per CU) or 1,024 (one block per CU, the same
 // 4 waves per SIMD): one LDS allocation per CU, whose 160 KB then cache
 // kPathsLdsNodesBig BVH4 nodes (the top ~5 levels) instead of 96.
-// 8 KB world + 8 B x kStack x 1,024 lanes of stacks + the node cache <= 160 KB (696 nodes at kStack 8)
-constexpr int kPathsLdsNodesBig = (160 * 1024 - 8192 - 8 * kPathsLdsStack * 1024 - 1024) / 128;
+// 8 KB world + 8 B x kStack x 1,024 lanes of stacks + the camera-ray rings (44 B
+// per lane) + the node cache <= 160 KB (344 nodes at kStack 8)
+constexpr int kPathsLdsNodesBig =
+    (160 * 1024 - 8192 - 8 * kPathsLdsStack * 1024 - 1024 - (SRR_RAYRING ? 4 * kRingWords * 1024 : 0)) / 128;
+// 256-lane blocks (4 per CU, <= 40 KB each): the ring displaces the node cache,
+// which only meshes use and these blocks serve mesh-free scenes (renderer.cpp)
+constexpr int kPathsLdsNodesSmall = SRR_RAYRING ? 8 : kPathsLdsNodes;
+
+// The camera ray of path index idx of the window (pixel-major: idx = lp * spp_w + s)
+// with its RNG streams, as k_paths' refill needs it.
+SRR_D void path_camera_ray(const SceneView& S, const PathWork& W, uint32_t idx, Ray& r, Rng& rng) {
+  const uint32_t lp = udiv31(idx, W.div_spp), s = idx - lp * (uint32_t)W.spp_w;
+  if ((int)lp >= W.npix || (int)s >= W.spp_w) atomicOr(W.err, 1);
+  const int pix = W.pixels ? W.pixels[lp] : lp;
+  V3 o, d;
+  float tm;
+  double sx, sy;
+  sobol2_point((uint32_t)(W.s_base + (int)s), sx, sy);  // = W.sobol[2 s], W.sobol[2 s + 1]
+  camera_ray(S, pix, W.s_base + s, sx, sy, W.nx, W.ny, W.base_seed, o, d, tm, rng, &W.div_nx);
+  r = Ray{o, d, tm};
+}
+
+template <int BS>
+SRR_D void ring_put(lds_ptr<float> e, const Ray& r, const Rng& rng) {  // e: the entry's word 0
+  e[0] = r.o.x;
+  e[BS] = r.o.y;
+  e[2 * BS] = r.o.z;
+  e[3 * BS] = r.d.x;
+  e[4 * BS] = r.d.y;
+  e[5 * BS] = r.d.z;
+  e[6 * BS] = r.tm;
+  e[7 * BS] = __uint_as_float((uint32_t)rng.lcg);
+  e[8 * BS] = __uint_as_float((uint32_t)(rng.lcg >> 32));
+  e[9 * BS] = __uint_as_float((uint32_t)rng.pcg);
+  e[10 * BS] = __uint_as_float((uint32_t)(rng.pcg >> 32));
+}
+
+template <int BS>
+SRR_D void ring_get(lds_ptr<const float> e, Ray& r, Rng& rng) {
+  r = Ray{v3(e[0], e[BS], e[2 * BS]), v3(e[3 * BS], e[4 * BS], e[5 * BS]), e[6 * BS]};
+  rng.lcg = (uint64_t)__float_as_uint(e[7 * BS]) | ((uint64_t)__float_as_uint(e[8 * BS]) << 32);
+  rng.pcg = (uint64_t)__float_as_uint(e[9 * BS]) | ((uint64_t)__float_as_uint(e[10 * BS]) << 32);
+}
 
 template <bool MEDIA, bool ALLFAM, int MINB, bool TIMED = false, bool WL = true, bool QUAD = false, bool CMP = false,
           bool CQ = false, int BS = kPathsBlock>
@@ -2532,7 +2589,8 @@ __global__ void __launch_bounds__(BS, MINB) k_paths(SceneView S0, PathWork W) {
   }
   __shared__ int s_node[kStack * BS];
   __shared__ float s_t[kStack * BS];
-  constexpr int kNodesLds = CMP ? kPathsLdsNodesCmp : (BS == 1024 ? kPathsLdsNodesBig : kPathsLdsNodes);
+  constexpr bool RING = SRR_RAYRING && !CMP;
+  constexpr int kNodesLds = CMP ? kPathsLdsNodesCmp : (BS == 1024 ? kPathsLdsNodesBig : kPathsLdsNodesSmall);
   // (CQ: the same LDS bytes hold twice as many 64-B nodes)
   const int n_lds_nodes = CQ ? min(S0.node4_total, 2 * kNodesLds) : min(S0.node4_total, kNodesLds);
   __shared__ float4 s_n4[kNodesLds * 8];
@@ -2544,6 +2602,11 @@ __global__ void __launch_bounds__(BS, MINB) k_paths(SceneView S0, PathWork W) {
   // (in) / hit t (out), triangle (out); per-wave queue counts | active bit
   __shared__ float s_q[CMP ? 8 * kPathsBlock : 1];
   __shared__ int s_wc[CMP ? kPathsBlock / 64 : 1];
+  // RING: the wave's camera-ray ring, SoA [kRingWords][BS]; the wave's 64 entries
+  // are its own lanes' columns (entry e of wave v at column 64 v + e)
+  __shared__ float s_ring[RING ? kRingWords * BS : 1];
+  const lds_ptr<float> ringw = to_lds(s_ring + (RING ? (threadIdx.x & ~63u) : 0));
+  uint32_t ring_base = 0;  // path index of the ring's entry 0 (wave-uniform)
   __syncthreads();
   TraceCtx cx{nullptr, to_lds(s_node + threadIdx.x), to_lds(s_t + threadIdx.x)};
   cx.lds_nodes = (const __attribute__((address_space(3))) f32x4*)to_lds(s_n4);
@@ -2585,8 +2648,54 @@ __global__ void __launch_bounds__(BS, MINB) k_paths(SceneView S0, PathWork W) {
       const uint32_t cnt = __popcll(nm);
       const uint32_t rank = __popcll(nm & ((1ull << lane_id()) - 1));
       const uint32_t avail = pool_end - pool;
-      uint32_t idx;
-      if (avail >= cnt) {
+      uint32_t idx = 0;
+      if (RING) {
+        // lanes whose path is in the ring's chunk take it first (before the chunk is replaced)
+        if (need && rank < avail) {
+          const uint32_t i0 = pool + rank;
+          if (i0 < n_paths) {
+            g = (int)i0;
+            ring_get<BS>(ringw + (i0 - ring_base), r, rng);
+            depth = 0;
+          }
+        }
+        if (avail >= cnt) {
+          pool += cnt;
+        } else {
+          uint32_t nb;
+          if (nxt_armed) {
+            nb = nxt_ready ? nxt_base : __builtin_amdgcn_readfirstlane(nxt_lane0);
+            nxt_armed = false;
+            nxt_ready = false;
+          } else {
+            uint32_t b = 0;
+            if (lane_id() == 0) b = (uint32_t)atomicAdd(W.cursor, (unsigned long long)kPoolChunk);
+            nb = __builtin_amdgcn_readfirstlane(b);
+          }
+          // the next chunk's camera rays, one per lane, every lane of the wave
+          const uint32_t gi = nb + (uint32_t)lane_id();
+          if (gi < n_paths) {
+            Ray gr;
+            Rng grng;
+            path_camera_ray(S, W, gi, gr, grng);
+            ring_put<BS>(ringw + lane_id(), gr, grng);
+          }
+          // (one wave writes and reads these entries: its LDS operations run in order;
+          // the fence keeps the compiler from moving the reads above the writes)
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+          ring_base = nb;
+          if (need && rank >= avail) {
+            const uint32_t i1 = nb + (rank - avail);
+            if (i1 < n_paths) {
+              g = (int)i1;
+              ring_get<BS>(ringw + (i1 - nb), r, rng);
+              depth = 0;
+            }
+          }
+          pool = nb + (cnt - avail);
+          pool_end = nb + (uint32_t)kPoolChunk;
+        }
+      } else if (avail >= cnt) {
         idx = pool + rank;
         pool += cnt;
       } else {
@@ -2604,18 +2713,9 @@ __global__ void __launch_bounds__(BS, MINB) k_paths(SceneView S0, PathWork W) {
         pool = nb + (cnt - avail);
         pool_end = nb + (uint32_t)kPoolChunk;
       }
-      if (need && idx < n_paths) {
+      if (!RING && need && idx < n_paths) {
         g = (int)idx;
-        // pixel-major: g = lp * spp_w + s
-        const uint32_t lp = udiv31(idx, W.div_spp), s = idx - lp * (uint32_t)W.spp_w;
-        if ((int)lp >= W.npix || (int)s >= W.spp_w) atomicOr(W.err, 1);
-        const int pix = W.pixels ? W.pixels[lp] : lp;
-        V3 o, d;
-        float tm;
-        double sx, sy;
-        sobol2_point((uint32_t)(W.s_base + (int)s), sx, sy);  // = W.sobol[2 s], W.sobol[2 s + 1]
-        camera_ray(S, pix, W.s_base + s, sx, sy, W.nx, W.ny, W.base_seed, o, d, tm, rng, &W.div_nx);
-        r = Ray{o, d, tm};
+        path_camera_ray(S, W, idx, r, rng);
         depth = 0;
       }
     }
