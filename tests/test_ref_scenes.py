@@ -20,6 +20,7 @@ import pytest
 import meshfiles as mf
 import oracle_bind as ob
 import parity
+import ref_fixtures
 from srr import capi, ref_scenes
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -44,8 +45,40 @@ def test_restated_builder_matches_reference(key):
     got = ob.render(sc.text(), m["nx"], m["ny"], m["spp"], m["max_depth"])
     want_paths, want_rays = _golden(key, m)
     pc = parity.compare_paths(got["paths"], want_paths)
-    assert pc["match"] >= parity.MIN_MATCH, pc
+    assert pc["bitexact"] == 1.0, pc  # every path, bit for bit
+    assert (got["rays"].reshape(want_rays.shape) == want_rays).all()  # and every path's world rays
     assert int(got["rays"].sum()) == m["world_rays"] == int(want_rays.sum())
+
+
+# ------------------------------------------- the goldens without /root/reference
+@pytest.mark.parametrize("key", ref_fixtures.KEYS)
+def test_fixture_scenes_render_the_reference_goldens(key):
+    """The committed fixture scenes (tests/ref_fixtures.py) through the CPU
+    restatement equal the REFERENCE's goldens: pins the fixtures the GPU test
+    below renders, on any host."""
+    m = META[key]
+    got = ob.render(ref_fixtures.scene_text(key), m["nx"], m["ny"], m["spp"], m["max_depth"])
+    want_paths, want_rays = _golden(key, m)
+    pc = parity.compare_paths(got["paths"], want_paths)
+    assert pc["bitexact"] == 1.0, pc
+    assert (got["rays"].reshape(want_rays.shape) == want_rays).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key", ref_fixtures.KEYS)
+def test_gpu_renders_the_reference_goldens(key):
+    """The HIP path against the goldens the REFERENCE rendered from its own builder
+    functions (refb_*) or classes (reft_*): every path and its world rays bit for
+    bit (the reference goldens had never run on the GPU)."""
+    m = META[key]
+    out = capi.Renderer(ref_fixtures.scene_text(key), device=0).render(m["nx"], m["ny"], m["spp"], m["max_depth"],
+                                                                       keep_paths=True)
+    want_paths, want_rays = _golden(key, m)
+    pc = parity.compare_paths(out["paths"].reshape(want_paths.shape), want_paths)
+    print(key, pc)
+    assert pc["bitexact"] == 1.0, (key, pc)
+    assert (out["rays"].reshape(want_rays.shape) == want_rays).all()
+    assert int(out["stats"]["world_rays"]) == m["world_rays"]
 
 
 def test_sceneid_table():
