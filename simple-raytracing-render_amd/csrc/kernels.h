@@ -122,7 +122,6 @@ struct PathWork {
   int gstack_cap;
   unsigned long long* wave_times;  // diagnostics (SRR_WAVE_TIMES): per wave [start, exit] s_memrealtime, or nullptr
   int deep_tries;         // coop_mixture: failed attempts after which a path takes every free lane (32)
-  int dbg;                // A/B diagnostics (SRR_PATHS_DBG), 0 in production
   float* slow_rays;       // diagnostics build (-DSRR_SLOW_RAYS=ticks): [65536][16] records of slow world hits
   unsigned* slow_count;
 };

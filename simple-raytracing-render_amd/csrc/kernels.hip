@@ -2483,16 +2483,6 @@ SRR_D float4 rec_load(const float4* p) { return SRR_REC_NT ? ntl(p) : *p; }
 constexpr int kPathsBlock = 256;
 constexpr unsigned long long kPoolChunk = 64;  // path indices a wave takes per cursor atomic
 
-// CMP: block-level compaction of the mesh traversal (scenes whose world list
-// holds one mesh at top level, SceneView::mesh_obj).  Each wave-iteration, every
-// lane tests the objects before the mesh and the mesh's root box (the
-// reference's bvh_node root, which contains every leaf box: a miss there is the
-// reference's miss, bvh.h:66); the block's lanes whose ray enters append it to
-// an LDS queue, the queue is traversed densely by the block's first lanes, and
-// each owner takes its result back and tests the objects after the mesh.  The
-// result of every ray is mesh_hit4's, so paths stay bit-identical.
-constexpr int kPathsLdsNodesCmp = 56;  // LDS node cache of the CMP variant (room for the queue)
-
 // Camera-ray ring (SRR_RAYRING, default on).  A lane whose path ended used to
 // generate its next camera ray itself (pixel and sample from the path index,
 // per-path seeds, Sobol point, lens disk, normalisation: a few hundred VALU
@@ -2506,6 +2496,10 @@ constexpr int kPathsLdsNodesCmp = 56;  // LDS node cache of the CMP variant (roo
 // path's ray is the same function of its index, so paths are unchanged.
 #ifndef SRR_RAYRING
 #define SRR_RAYRING 1
+#endif
+// diagnostics-only k_paths variants (phase timing, compressed nodes): `make diag`
+#ifndef SRR_DIAG_VARIANTS
+#define SRR_DIAG_VARIANTS 0
 #endif
 constexpr int kRingWords = 11;  // o.xyz, d.xyz, time, lcg (2 words), pcg (2 words)
 
@@ -2556,70 +2550,90 @@ SRR_D void ring_get(lds_ptr<const float> e, Ray& r, Rng& rng) {
   rng.pcg = (uint64_t)__float_as_uint(e[9 * BS]) | ((uint64_t)__float_as_uint(e[10 * BS]) << 32);
 }
 
-template <bool MEDIA, bool ALLFAM, int MINB, bool TIMED = false, bool WL = true, bool QUAD = false, bool CMP = false,
-          bool CQ = false, int BS = kPathsBlock>
-__global__ void __launch_bounds__(BS, MINB) k_paths(SceneView S0, PathWork W) {
-  static_assert(!CMP || (!MEDIA && !TIMED && WL && !QUAD && BS == kPathsBlock),
-                "CMP: world list in LDS, no media, per-lane walks, 256-lane blocks");
+// k_paths' arguments, read through the kernel-argument segment pointer laundered
+// by an empty asm (paths_args): the compiler can no longer prove two reads of a
+// field equal, so each phase of the path loop (refill, world hit, record and
+// scatter, mixture, fold) loads the fields it uses with scalar loads at its start
+// and they die at its end.  With the arguments as one by-value SceneView /
+// PathWork, every table pointer of the scene and the window (~40 64-bit values)
+// stayed live in SGPRs across the whole loop, and 114-137 of them spilled to VGPR
+// lanes: each reload a v_readlane on the VALU, and in the 128-VGPR ALLFAM / MEDIA
+// variants those VGPRs spilled on to scratch memory.
+struct PathsArgs {
+  SceneView S;
+  PathWork W;
+};
+#if defined(__HIP_DEVICE_COMPILE__)
+template <class T>
+using kptr = const __attribute__((address_space(4))) T*;
+SRR_D kptr<PathsArgs> paths_args() {
+  kptr<PathsArgs> p = (kptr<PathsArgs>)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return p;
+}
+#else  // (the host pass parses kernel bodies but never compiles them)
+SRR_D const PathsArgs* paths_args() { return nullptr; }
+#endif
+
+template <bool MEDIA, bool ALLFAM, int MINB, bool TIMED = false, bool WL = true, bool QUAD = false, bool CQ = false,
+          int BS = kPathsBlock>
+__global__ void __launch_bounds__(BS, MINB) k_paths(PathsArgs A) {
   static_assert(BS == kPathsBlock || BS == 1024, "block size");
+  (void)A;  // read through paths_args()
   // TIMED (diagnostics): per-wave cycles in refill / world hit (mesh part) / record+scatter / fold
   uint64_t tp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t it = 0;
-  const uint64_t t_start = W.wave_times ? __builtin_amdgcn_s_memrealtime() : 0;
-  SceneView S = S0;
   // WL: world tables staged in LDS (they fit in kWorldLdsBytes); otherwise read
   // from global memory (large object lists, e.g. random_scene's ~490 spheres)
   // QUAD: meshes traced by mesh_hit4_quad (large BVHs, SceneView::quad_trace)
   constexpr int TR = TR_BVH4_PRUNE | (WL ? TR_WL : 0) | (QUAD ? TR_QUAD : 0) | (CQ ? TR_Q : 0) | (BS == 1024 ? TR_BIG : 0);
-  if constexpr (WL) {
-    __shared__ uint4 s_world[kWorldLdsBytes / 16];
-    for (int i = threadIdx.x; i < S0.world_words; i += blockDim.x) s_world[i] = S0.world_blob[i];
-    __syncthreads();
-    const char* b = (const char*)s_world;
-    S.objs = (const DObj*)(b + S0.world_off[0]);
-    S.xforms = (const DXform*)(b + S0.world_off[1]);
-    S.spheres = (const DSphere*)(b + S0.world_off[2]);
-    S.rects = (const DRect*)(b + S0.world_off[3]);
-    S.stris = (const DStandaloneTri*)(b + S0.world_off[4]);
-    S.meshes = (const DMesh*)(b + S0.world_off[5]);
-    S.media = (const DMedium*)(b + S0.world_off[6]);
-    S.mats = (const DMat*)(b + S0.world_off[7]);
-    S.texs = (const DTex*)(b + S0.world_off[8]);
-    S.lights = (const DLight*)(b + S0.world_off[9]);
-  }
+  __shared__ uint4 s_world[WL ? kWorldLdsBytes / 16 : 1];
+  // the scene as a phase reads it: scalar loads of the fields it uses, the world
+  // tables re-pointed into LDS (WL)
+  const auto view = [&]() {
+    SceneView S = paths_args()->S;
+    if constexpr (WL) {
+      const char* b = (const char*)s_world;
+      S.objs = (const DObj*)(b + S.world_off[0]);
+      S.xforms = (const DXform*)(b + S.world_off[1]);
+      S.spheres = (const DSphere*)(b + S.world_off[2]);
+      S.rects = (const DRect*)(b + S.world_off[3]);
+      S.stris = (const DStandaloneTri*)(b + S.world_off[4]);
+      S.meshes = (const DMesh*)(b + S.world_off[5]);
+      S.media = (const DMedium*)(b + S.world_off[6]);
+      S.mats = (const DMat*)(b + S.world_off[7]);
+      S.texs = (const DTex*)(b + S.world_off[8]);
+      S.lights = (const DLight*)(b + S.world_off[9]);
+    }
+    return S;
+  };
+  const auto work = []() { return PathWork(paths_args()->W); };
   __shared__ int s_node[kStack * BS];
   __shared__ float s_t[kStack * BS];
-  constexpr bool RING = SRR_RAYRING && !CMP;
-  constexpr int kNodesLds = CMP ? kPathsLdsNodesCmp : (BS == 1024 ? kPathsLdsNodesBig : kPathsLdsNodesSmall);
-  // (CQ: the same LDS bytes hold twice as many 64-B nodes)
-  const int n_lds_nodes = CQ ? min(S0.node4_total, 2 * kNodesLds) : min(S0.node4_total, kNodesLds);
+  constexpr bool RING = SRR_RAYRING;
+  constexpr int kNodesLds = BS == 1024 ? kPathsLdsNodesBig : kPathsLdsNodesSmall;
   __shared__ float4 s_n4[kNodesLds * 8];
-  if (CQ)
-    for (int i = threadIdx.x; i < n_lds_nodes * 4; i += blockDim.x) s_n4[i] = S0.node4q[i];
-  else
-    for (int i = threadIdx.x; i < n_lds_nodes * 8; i += blockDim.x) s_n4[i] = S0.node4[i];
-  // CMP: the mesh-ray queue, SoA [8][kPathsBlock]: origin, direction, t bound
-  // (in) / hit t (out), triangle (out); per-wave queue counts | active bit
-  __shared__ float s_q[CMP ? 8 * kPathsBlock : 1];
-  __shared__ int s_wc[CMP ? kPathsBlock / 64 : 1];
   // RING: the wave's camera-ray ring, SoA [kRingWords][BS]; the wave's 64 entries
   // are its own lanes' columns (entry e of wave v at column 64 v + e)
   __shared__ float s_ring[RING ? kRingWords * BS : 1];
   const lds_ptr<float> ringw = to_lds(s_ring + (RING ? (threadIdx.x & ~63u) : 0));
   uint32_t ring_base = 0;  // path index of the ring's entry 0 (wave-uniform)
+  const uint32_t n_paths = (uint32_t)paths_args()->W.n_paths;
+  const uint64_t t_start = paths_args()->W.wave_times ? __builtin_amdgcn_s_memrealtime() : 0;
+  {
+    const SceneView S0 = paths_args()->S;
+    if constexpr (WL)
+      for (int i = threadIdx.x; i < S0.world_words; i += blockDim.x) s_world[i] = S0.world_blob[i];
+    // (CQ: the same LDS bytes hold twice as many 64-B nodes)
+    const int n_lds_nodes = CQ ? min(S0.node4_total, 2 * kNodesLds) : min(S0.node4_total, kNodesLds);
+    if (CQ)
+      for (int i = threadIdx.x; i < n_lds_nodes * 4; i += blockDim.x) s_n4[i] = S0.node4q[i];
+    else
+      for (int i = threadIdx.x; i < n_lds_nodes * 8; i += blockDim.x) s_n4[i] = S0.node4[i];
+  }
   __syncthreads();
-  TraceCtx cx{nullptr, to_lds(s_node + threadIdx.x), to_lds(s_t + threadIdx.x)};
-  cx.lds_nodes = (const __attribute__((address_space(3))) f32x4*)to_lds(s_n4);
-  cx.lds_count = n_lds_nodes;
-  cx.st_cap = W.stack_cap;
-  cx.ovf = W.counters + 11;
-  cx.gst = W.gstack;
-  cx.gst_cap = W.gstack ? W.gstack_cap : 0;
-  cx.gst_stride = W.lanes;
   const int slot = blockIdx.x * blockDim.x + threadIdx.x;
-  cx.slot = slot;
   int g = -1;  // path of this lane (a window numbers its paths below 2^31), -1 idle
-  const uint32_t n_paths = (uint32_t)W.n_paths;
   // the wave's unissued path indices [pool, pool_end): wave-uniform (scalar)
   uint32_t pool = 0, pool_end = 0;
   uint32_t nxt_lane0 = 0;  // lane 0: base of the armed next chunk
@@ -2645,6 +2659,8 @@ __global__ void __launch_bounds__(BS, MINB) k_paths(SceneView S0, PathWork W) {
     const bool need = g < 0;
     const uint64_t nm = __ballot(need);
     if (nm && pool < n_paths) {
+      const SceneView S = view();
+      const PathWork W = work();
       const uint32_t cnt = __popcll(nm);
       const uint32_t rank = __popcll(nm & ((1ull << lane_id()) - 1));
       const uint32_t avail = pool_end - pool;
@@ -2720,16 +2736,15 @@ __global__ void __launch_bounds__(BS, MINB) k_paths(SceneView S0, PathWork W) {
       }
     }
     if (!nxt_armed && pool_end < n_paths) {  // arm the next chunk
-      if (lane_id() == 0) nxt_lane0 = (uint32_t)atomicAdd(W.cursor, (unsigned long long)kPoolChunk);
+      if (lane_id() == 0) nxt_lane0 = (uint32_t)atomicAdd(paths_args()->W.cursor, (unsigned long long)kPoolChunk);
       nxt_armed = true;
     }
-    if (!CMP && __ballot(g >= 0) == 0) break;  // (CMP: the block leaves together, below)
+    if (__ballot(g >= 0) == 0) break;
     if (TIMED) {
       __builtin_amdgcn_s_waitcnt(0);
       const uint64_t t = __builtin_amdgcn_s_memtime();
       tp[0] += t - tq;
       tq = t;
-      cx.mesh_cycles = 0;
       ++it;
     }
     bool done = false;
@@ -2743,80 +2758,24 @@ __global__ void __launch_bounds__(BS, MINB) k_paths(SceneView S0, PathWork W) {
     int d_tries = 0;
     bool d_dead = false;
     WorldHit w{-1, -1, 0};
-    if constexpr (CMP) {
-      const int mk = S0.mesh_obj;
-      const DObj mob = S.objs[mk];
-      const DMesh mm = S.meshes[mob.idx];
-      float closest = FLT_MAX;  // Raytracing_n.cpp:58
-      bool want = false;
-      Ray lr{};
-      if (g >= 0) {
-        world_objs<false, TR>(S, r, rng, cx, 0, mk, w, closest);
-        lr = chain_in<TR>(S, mob, r);
-        const V3 inv = v3(1.0f / lr.d.x, 1.0f / lr.d.y, 1.0f / lr.d.z);
-        // W.dbg (A/B diagnostics): bit 0 queues every ray (no root-box test);
-        // bit 1 walks in-lane (the variant's barriers without the compaction)
-        want = (W.dbg & 1) ? true : slab(S0.nodes[2 * mm.node_off], S0.nodes[2 * mm.node_off + 1], lr.o, inv, 0.001f, closest);
-        if (want && (W.dbg & 2)) {
-          MeshHit mh;
-          if (mesh_hit4<true>(S, mm, lr, 0.001f, closest, false, mh, cx)) {
-            closest = mh.t;
-            w = WorldHit{mk, mh.tri, closest};
-          }
-          want = false;
-        }
-      }
-      const uint64_t wm = __ballot(want);
-      const bool wave_busy = __ballot(g >= 0) != 0;  // (ballots outside the lane-0 branch: all lanes vote)
-      const int wv = threadIdx.x >> 6;
-      if (lane_id() == 0) s_wc[wv] = __popcll(wm) | (wave_busy ? 0x10000 : 0);
-      __syncthreads();
-      int base = 0, nq = 0, act = 0;
-#pragma unroll
-      for (int k = 0; k < kPathsBlock / 64; ++k) {
-        const int c = s_wc[k];
-        base += k < wv ? (c & 0xffff) : 0;
-        nq += c & 0xffff;
-        act |= c >> 16;
-      }
-      if (!act) break;  // every lane of the block is out of paths (block-uniform)
-      const int qi = base + __popcll(wm & ((1ull << lane_id()) - 1));
-      if (want) {
-        s_q[qi] = lr.o.x;
-        s_q[kPathsBlock + qi] = lr.o.y;
-        s_q[2 * kPathsBlock + qi] = lr.o.z;
-        s_q[3 * kPathsBlock + qi] = lr.d.x;
-        s_q[4 * kPathsBlock + qi] = lr.d.y;
-        s_q[5 * kPathsBlock + qi] = lr.d.z;
-        s_q[6 * kPathsBlock + qi] = closest;
-      }
-      __syncthreads();
-      if ((int)threadIdx.x < nq) {  // the queue, densely: waves 0 .. ceil(nq / 64) - 1
-        const int i = threadIdx.x;
-        const Ray qr{v3(s_q[i], s_q[kPathsBlock + i], s_q[2 * kPathsBlock + i]),
-                     v3(s_q[3 * kPathsBlock + i], s_q[4 * kPathsBlock + i], s_q[5 * kPathsBlock + i]), 0.f};
-        MeshHit mh;
-        const bool f = mesh_hit4<true>(S, mm, qr, 0.001f, s_q[6 * kPathsBlock + i], false, mh, cx);
-        s_q[6 * kPathsBlock + i] = mh.t;
-        s_q[7 * kPathsBlock + i] = __int_as_float(f ? mh.tri : -1);
-      }
-      __syncthreads();
-      if (want) {
-        const int tri = __float_as_int(s_q[7 * kPathsBlock + qi]);
-        if (tri >= 0) {
-          closest = s_q[6 * kPathsBlock + qi];
-          w = WorldHit{mk, tri, closest};
-        }
-      }
-      if (g >= 0) world_objs<false, TR>(S, r, rng, cx, mk + 1, S.n_world, w, closest);
-    }
     if (g >= 0) {
+      const SceneView S = view();
+      const PathWork W = work();
+      TraceCtx cx{nullptr, to_lds(s_node + threadIdx.x), to_lds(s_t + threadIdx.x)};
+      cx.lds_nodes = (const __attribute__((address_space(3))) f32x4*)to_lds(s_n4);
+      cx.lds_count = CQ ? min(S.node4_total, 2 * kNodesLds) : min(S.node4_total, kNodesLds);
+      cx.st_cap = W.stack_cap;
+      cx.ovf = W.counters + 11;
+      cx.gst = W.gstack;
+      cx.gst_cap = W.gstack ? W.gstack_cap : 0;
+      cx.gst_stride = W.lanes;
+      cx.slot = slot;
 #ifdef SRR_SLOW_RAYS
       const uint64_t t_w0 = __builtin_amdgcn_s_memrealtime();
       cx.last_steps = 0;
       const Ray r_in = r;
 #endif
-      if constexpr (!CMP) w = world_hit<MEDIA, TIMED ? (TR_BVH4_TIMED | (WL ? TR_WL : 0)) : TR>(S, r, rng, cx);
+      w = world_hit<MEDIA, TIMED ? (TR_BVH4_TIMED | (WL ? TR_WL : 0)) : TR>(S, r, rng, cx);
 #ifdef SRR_SLOW_RAYS
       // diagnostics build: every lane of a world hit slower than SRR_SLOW_RAYS
       // ticks (100 MHz) records its ray: g, depth, o, d, time, ticks, steps, hit
@@ -2854,6 +2813,8 @@ __global__ void __launch_bounds__(BS, MINB) k_paths(SceneView S0, PathWork W) {
     }
     if (g >= 0) {
       if (w.obj >= 0) {
+        const SceneView S = view();
+        const PathWork W = work();
         const HitRec h = world_record<TR>(S, r, w);
         const int kind = h.mat >= 0 ? S.mats[h.mat].kind : -1;
         if (TIMED) {
@@ -2901,6 +2862,7 @@ __global__ void __launch_bounds__(BS, MINB) k_paths(SceneView S0, PathWork W) {
       }
     }
     if (__ballot(pend)) {
+      const SceneView S = view();
       const uint64_t tc = TIMED ? __builtin_amdgcn_s_memtime() : 0;
       // SRR_MIXTURE_SKIP 1: per-lane loops passing over dead draws; 2: one such
       // round, then the wave-cooperative loop for what is left; 0: cooperative only
@@ -2909,10 +2871,7 @@ __global__ void __launch_bounds__(BS, MINB) k_paths(SceneView S0, PathWork W) {
         rounds = skip_mixture(S, ds, d_dead, pend, d_tries, rng.lcg, d_dir, d_pdf);
       } else {
         if (SRR_MIXTURE_SKIP == 2) rounds = skip_mixture(S, ds, d_dead, pend, d_tries, rng.lcg, d_dir, d_pdf, 1);
-#ifdef SRR_EXP_MIX1  // timing experiment only (wrong image): one attempt per loop
-        if (pend) { pend = false; d_pdf = 1.f; }
-#endif
-        if (__ballot(pend)) rounds += coop_mixture(S, ds, pend, d_tries, rng.lcg, d_dir, d_pdf, W.deep_tries);
+        if (__ballot(pend)) rounds += coop_mixture(S, ds, pend, d_tries, rng.lcg, d_dir, d_pdf, paths_args()->W.deep_tries);
       }
       if (TIMED) {
         tp[6] += __builtin_amdgcn_s_memtime() - tc;
@@ -2921,6 +2880,7 @@ __global__ void __launch_bounds__(BS, MINB) k_paths(SceneView S0, PathWork W) {
       max_rounds = max(max_rounds, (uint32_t)rounds);
     }
     if (diff) {  // the rest of scatter<FAM_DIFF>: scattering_pdf and the record
+      const PathWork W = work();
       if (d_pdf == 0) ++n_capped;  // the loop reached kMixtureGuard
       float c = dot(d_n, unit_vector(d_dir));  // material.h:100-105, 134-138
       if (c < 0) c = 0;
@@ -2931,6 +2891,7 @@ __global__ void __launch_bounds__(BS, MINB) k_paths(SceneView S0, PathWork W) {
       ++depth;
     }
     if (g >= 0) {
+      const PathWork W = work();
       if (TIMED) {
         const uint64_t t = __builtin_amdgcn_s_memtime();
         tp[3] += t - tq;
@@ -2968,6 +2929,7 @@ __global__ void __launch_bounds__(BS, MINB) k_paths(SceneView S0, PathWork W) {
       if (TIMED) tp[4] += __builtin_amdgcn_s_memtime() - tq;
     }
   }
+  const PathWork W = work();
   if (TIMED && lane_id() == 0) {  // per-wave totals -> W.counters[4..9]
     for (int q = 0; q < 5; ++q) atomicAdd(W.counters + 4 + q, (unsigned long long)tp[q]);
     atomicAdd(W.counters + 9, (unsigned long long)it);
@@ -3565,13 +3527,13 @@ int paths_lanes_per_device(const SceneView& S, int device) {
 }
 
 void launch_paths(const SceneView& S, const PathWork& W, int all_families, hipStream_t st) {
+  const dev::PathsArgs args{S, W};
   const int blocks = W.lanes / dev::kPathsBlock;
-  static const bool timed = getenv("SRR_PATHS_TIMING") != nullptr;
   static const bool force_global = getenv("SRR_WORLD_GLOBAL") != nullptr;  // A/B diagnostics
   if (force_global || S.world_words * 16 > dev::kWorldLdsBytes) {  // world tables too large for LDS: global reads
 #define SRR_LAUNCH_PATHS_G(M, A)                                                                                      \
-  if (S.quad_trace) hipLaunchKernelGGL((dev::k_paths<M, A, 4, false, false, true>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W); \
-  else hipLaunchKernelGGL((dev::k_paths<M, A, 4, false, false>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W)
+  if (S.quad_trace) hipLaunchKernelGGL((dev::k_paths<M, A, 4, false, false, true>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, args); \
+  else hipLaunchKernelGGL((dev::k_paths<M, A, 4, false, false>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, args)
     if (S.has_media) {
       if (all_families) SRR_LAUNCH_PATHS_G(true, true);
       else SRR_LAUNCH_PATHS_G(true, false);
@@ -3582,23 +3544,27 @@ void launch_paths(const SceneView& S, const PathWork& W, int all_families, hipSt
 #undef SRR_LAUNCH_PATHS_G
     return;
   }
-  // opt-in (SRR_COMPACT=1): measured 20 % slower on C2
-  static const bool compact = [] {
-    const char* e = getenv("SRR_COMPACT");
-    return e && atoi(e) != 0;
-  }();
-  const bool cmp = compact && S.mesh_obj >= 0 && !S.has_media && !S.quad_trace && !timed;
-  const bool cq = S.use_q && !S.quad_trace && !timed && !cmp;  // compressed nodes, per-lane walks
   const int bs = paths_block_lanes(S);
   const int blocks_b = W.lanes / bs;
+#if SRR_DIAG_VARIANTS
+  // diagnostics build (make diag): SRR_PATHS_TIMING=1 phase timing, SRR_CBVH=1 compressed nodes
+  static const bool timed = getenv("SRR_PATHS_TIMING") != nullptr;
+  const bool cq = S.use_q && !S.quad_trace && !timed;  // compressed nodes, per-lane walks
+#define SRR_LAUNCH_PATHS_DIAG(M, A, B)                                                                                         \
+  if (timed) hipLaunchKernelGGL((dev::k_paths<M, A, 4, true>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, args);           \
+  else if (bs == 1024 && B == 4 && cq) hipLaunchKernelGGL((dev::k_paths<M, A, 4, false, true, false, true, 1024>), dim3(blocks_b), dim3(1024), 0, st, args); \
+  else if (cq && B == 4) hipLaunchKernelGGL((dev::k_paths<M, A, 4, false, true, false, true>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, args); \
+  else
+#else
+  if (S.use_q || getenv("SRR_PATHS_TIMING"))
+    fprintf(stderr, "srr: SRR_CBVH / SRR_PATHS_TIMING need the diagnostics build (make diag); ignored\n");
+#define SRR_LAUNCH_PATHS_DIAG(M, A, B)
+#endif
 #define SRR_LAUNCH_PATHS(M, A, B)                                                                      \
-  if (timed) hipLaunchKernelGGL((dev::k_paths<M, A, 4, true>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W); \
-  else if (!M && cmp && B == 4) hipLaunchKernelGGL((dev::k_paths<false, A, 4, false, true, false, true>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W); \
-  else if (bs == 1024 && B == 4 && cq) hipLaunchKernelGGL((dev::k_paths<M, A, 4, false, true, false, false, true, 1024>), dim3(blocks_b), dim3(1024), 0, st, S, W); \
-  else if (bs == 1024 && B == 4 && !S.quad_trace) hipLaunchKernelGGL((dev::k_paths<M, A, 4, false, true, false, false, false, 1024>), dim3(blocks_b), dim3(1024), 0, st, S, W); \
-  else if (cq && B == 4) hipLaunchKernelGGL((dev::k_paths<M, A, 4, false, true, false, false, true>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W); \
-  else if (S.quad_trace && B == 4) hipLaunchKernelGGL((dev::k_paths<M, A, 4, false, true, true>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W); \
-  else hipLaunchKernelGGL((dev::k_paths<M, A, B>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, S, W)
+  SRR_LAUNCH_PATHS_DIAG(M, A, B)                                                                       \
+  if (bs == 1024 && B == 4 && !S.quad_trace) hipLaunchKernelGGL((dev::k_paths<M, A, 4, false, true, false, false, 1024>), dim3(blocks_b), dim3(1024), 0, st, args); \
+  else if (S.quad_trace && B == 4) hipLaunchKernelGGL((dev::k_paths<M, A, 4, false, true, true>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, args); \
+  else hipLaunchKernelGGL((dev::k_paths<M, A, B>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, args)
 #ifdef SRR_OCC_VARIANTS  // occupancy A/B builds (SRR_PATHS_OCC): 2, 3, 5 and 6 blocks per CU
 #define SRR_LAUNCH_PATHS_B(M, A)                          \
   switch (paths_min_blocks()) {                           \
@@ -3618,6 +3584,7 @@ void launch_paths(const SceneView& S, const PathWork& W, int all_families, hipSt
     if (all_families) { SRR_LAUNCH_PATHS_B(false, true) }
     else { SRR_LAUNCH_PATHS_B(false, false) }
   }
+#undef SRR_LAUNCH_PATHS_DIAG
 #undef SRR_LAUNCH_PATHS_B
 #undef SRR_LAUNCH_PATHS
 }

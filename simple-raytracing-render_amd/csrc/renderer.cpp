@@ -449,7 +449,6 @@ static int paths_enqueue(srr_renderer* r, FrameSlot& F, const srr_params* p, boo
     w.gstack_cap = gst_cap;
     w.wave_times = wave_times;
     w.deep_tries = deep_tries;
-    w.dbg = getenv("SRR_PATHS_DBG") ? atoi(getenv("SRR_PATHS_DBG")) : 0;
     w.slow_rays = diagnostics ? r->pw_slow : nullptr;
     w.slow_count = w.slow_rays ? (unsigned*)(r->pw_slow + 16 * 65536) : nullptr;
     const int wi = s0 / W;
