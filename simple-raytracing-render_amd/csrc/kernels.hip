@@ -2764,7 +2764,9 @@ __global__ void __launch_bounds__(BS, MINB) k_paths(PathsArgs A) {
       TraceCtx cx{nullptr, to_lds(s_node + threadIdx.x), to_lds(s_t + threadIdx.x)};
       cx.lds_nodes = (const __attribute__((address_space(3))) f32x4*)to_lds(s_n4);
       cx.lds_count = CQ ? min(S.node4_total, 2 * kNodesLds) : min(S.node4_total, kNodesLds);
-      cx.st_cap = W.stack_cap;
+      // (clamped: a host compiled with another SRR_KSTACK must not index past the
+      // kernel's kStack LDS entries per lane)
+      cx.st_cap = min(W.stack_cap, kStack);
       cx.ovf = W.counters + 11;
       cx.gst = W.gstack;
       cx.gst_cap = W.gstack ? W.gstack_cap : 0;
@@ -3501,17 +3503,12 @@ int paths_block_lanes(const SceneView& S) {
     const char* e = getenv("SRR_BIGBLOCK");
     return !e || atoi(e) != 0;
   }();
-  static const bool timed = getenv("SRR_PATHS_TIMING") != nullptr;
+  static const bool timed = SRR_DIAG_VARIANTS && getenv("SRR_PATHS_TIMING") != nullptr;
   static const bool force_global = getenv("SRR_WORLD_GLOBAL") != nullptr;
-  static const bool compact = [] {
-    const char* e = getenv("SRR_COMPACT");
-    return e && atoi(e) != 0;
-  }();
   const bool wl = !force_global && S.world_words * 16 <= dev::kWorldLdsBytes;
-  const bool cmp = compact && S.mesh_obj >= 0 && !S.has_media && !S.quad_trace;
   // (a scene without meshes has no BVH4 nodes to cache: 256-lane blocks, which
   // free their CU slots at a finer grain when frames overlap -- C1 +1.6 %)
-  return (big && wl && !timed && !cmp && !S.quad_trace && S.node4_total > 0 &&
+  return (big && wl && !timed && !S.quad_trace && S.node4_total > 0 &&
           paths_min_blocks() == kPathsOccDefault) ? 1024 : dev::kPathsBlock;
 }
 

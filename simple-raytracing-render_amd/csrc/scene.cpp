@@ -6,8 +6,10 @@
 #include "scene.h"
 
 #include <algorithm>
+#include <array>
 #include <cfloat>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
@@ -757,25 +759,206 @@ struct Flattener {
     build(0, (int)units.size());
     return T;
   }
+  // SAH cost weights of the 4-wide walk (mesh_hit4): one node step tests 4 child
+  // boxes; a leaf unit's 1-2 triangle tests cost kSahTri each.  Relative to the
+  // root's area, as probabilities of a random ray reaching a box.
+  static constexpr double kSahNode4 = 1.0, kSahNode2 = 0.5, kSahTri = 1.2;
+
+  static int leaf_tris(const TNode& n) { return (n.code & 1) + 1; }
+
+  // Treelet restructuring (Karras & Aila 2013) of the binary hierarchy over the
+  // fixed leaf units: every treelet of up to 7 nodes' subtrees (its "leaves" may be
+  // inner nodes) is rebuilt with the topology of least SAH cost, found by dynamic
+  // programming over the subsets of those subtrees; a few bottom-up passes.  Leaf
+  // units are never split or merged (they are the reference's leaves, whose slab
+  // tests decide which triangles the reference tests), so any topology is exact.
+  static void restructure(std::vector<TNode>& T, int root, int passes) {
+    const int N = (int)T.size();
+    std::vector<double> cost(N), area(N);
+    std::vector<int> parent(N, -1);
+    std::function<void(int)> eval = [&](int n) {
+      area[n] = box_area(T[n].box);
+      if (T[n].code >= 0) {
+        cost[n] = kSahTri * leaf_tris(T[n]) * area[n];
+        return;
+      }
+      parent[T[n].left] = n;
+      parent[T[n].right] = n;
+      eval(T[n].left);
+      eval(T[n].right);
+      cost[n] = kSahNode2 * area[n] + cost[T[n].left] + cost[T[n].right];
+    };
+    constexpr int K = 7;
+    for (int pass = 0; pass < passes; ++pass) {
+      eval(root);
+      // post-order list of inner nodes
+      std::vector<int> order;
+      std::function<void(int)> post = [&](int n) {
+        if (T[n].code >= 0) return;
+        post(T[n].left);
+        post(T[n].right);
+        order.push_back(n);
+      };
+      post(root);
+      for (int tr : order) {
+        // grow the treelet: repeatedly open the largest-area treelet leaf that is inner
+        std::vector<int> leaves{T[tr].left, T[tr].right}, inner{tr};
+        while ((int)leaves.size() < K) {
+          int best = -1;
+          double ba = -1;
+          for (int k = 0; k < (int)leaves.size(); ++k)
+            if (T[leaves[k]].code < 0 && area[leaves[k]] > ba) { ba = area[leaves[k]]; best = k; }
+          if (best < 0) break;
+          const int n = leaves[best];
+          inner.push_back(n);
+          leaves[best] = T[n].left;
+          leaves.push_back(T[n].right);
+        }
+        const int nl = (int)leaves.size();
+        if (nl < 3) continue;
+        const int full = (1 << nl) - 1;
+        std::vector<Box3> sbox(full + 1);
+        std::vector<double> sa(full + 1), copt(full + 1);
+        std::vector<int> split(full + 1, 0);
+        for (int sset = 1; sset <= full; ++sset) {
+          bool first = true;
+          for (int k = 0; k < nl; ++k)
+            if (sset >> k & 1) {
+              sbox[sset] = first ? T[leaves[k]].box : box_union(sbox[sset], T[leaves[k]].box);
+              first = false;
+            }
+          sa[sset] = box_area(sbox[sset]);
+        }
+        for (int k = 0; k < nl; ++k) copt[1 << k] = cost[leaves[k]];
+        for (int sset = 1; sset <= full; ++sset) {
+          if ((sset & (sset - 1)) == 0) continue;
+          double best = INFINITY;
+          int bsplit = 0;
+          // every split into two non-empty halves (each unordered pair once)
+          for (int p = (sset - 1) & sset; p > 0; p = (p - 1) & sset) {
+            const int q = sset ^ p;
+            if (p < q) continue;
+            const double c = copt[p] + copt[q];
+            if (c < best) { best = c; bsplit = p; }
+          }
+          copt[sset] = kSahNode2 * sa[sset] + best;
+          split[sset] = bsplit;
+        }
+        if (copt[full] + 1e-9 * copt[full] >= cost[tr]) continue;  // no better topology
+        // rebuild the treelet with the optimal topology, reusing its inner nodes
+        int next_inner = 1;  // inner[0] = tr stays the treelet root
+        std::function<int(int, int)> emit = [&](int sset, int node) -> int {
+          if ((sset & (sset - 1)) == 0) {
+            for (int k = 0; k < nl; ++k)
+              if (sset == (1 << k)) return leaves[k];
+          }
+          const int me = node >= 0 ? node : inner[next_inner++];
+          const int p = split[sset];
+          const int l = emit(p, -1), r = emit(sset ^ p, -1);
+          T[me].left = l;
+          T[me].right = r;
+          T[me].code = -1;
+          T[me].box = sbox[sset];
+          cost[me] = kSahNode2 * sa[sset] + cost[l] + cost[r];
+          area[me] = sa[sset];
+          return me;
+        };
+        emit(full, tr);
+      }
+    }
+  }
+
+  // SAH cost of the 4-wide hierarchy the collapse below makes of T (relative to
+  // the root area): node steps plus triangle tests, kSahNode4 / kSahTri weights
+  struct Collapse {
+    const std::vector<TNode>& T;
+    std::vector<std::array<double, 5>> f;  // f[n][k]: least cost of n's subtree as k slots
+    std::vector<std::array<int, 5>> pick;  // the left child's share of the k slots
+    explicit Collapse(const std::vector<TNode>& t) : T(t), f(t.size()), pick(t.size()) {
+      for (auto& a : f) a.fill(-1.0);
+    }
+    // one slot holding n: a leaf unit (its triangle tests) or a 4-wide node
+    double slot(int n) {
+      const TNode& t = T[n];
+      if (t.code >= 0) return kSahTri * leaf_tris(t) * box_area(t.box);
+      double best = INFINITY;
+      for (int k = 2; k <= 4; ++k) best = std::min(best, open(n, k));
+      return kSahNode4 * box_area(t.box) + best;
+    }
+    // n opened into exactly k slots (k >= 2) split between its children
+    double open(int n, int k) {
+      if (f[n][k] >= 0) return f[n][k];
+      const TNode& t = T[n];
+      double best = INFINITY;
+      int bi = 0;
+      for (int i = 1; i < k; ++i) {
+        const double c = slots(t.left, i) + slots(t.right, k - i);
+        if (c < best) { best = c; bi = i; }
+      }
+      pick[n][k] = bi;
+      return f[n][k] = best;
+    }
+    double slots(int n, int k) {  // n's subtree as exactly k slots
+      if (k == 1) return slot(n);
+      if (T[n].code >= 0) return INFINITY;
+      return open(n, k);
+    }
+    // the k slots chosen for n's subtree
+    void cut(int n, int k, std::vector<int>& out) {
+      if (k == 1) { out.push_back(n); return; }
+      open(n, k);
+      const int i = pick[n][k];
+      cut(T[n].left, i, out);
+      cut(T[n].right, k - i, out);
+    }
+    // the children of n as a 4-wide node: the best k in 2..4
+    std::vector<int> children(int n) {
+      int bk = 2;
+      double best = INFINITY;
+      for (int k = 2; k <= 4; ++k)
+        if (open(n, k) < best) { best = open(n, k); bk = k; }
+      std::vector<int> out;
+      cut(n, bk, out);
+      return out;
+    }
+  };
+
   void build_node4(const HBvh& B, DMesh& m) {
     static const bool ref_topology = [] {
       const char* e = getenv("SRR_BVH4");
       return e && !strcmp(e, "ref");
     }();
-    const std::vector<TNode> T = ref_topology ? tree_from_reference(B, m.tri_off) : tree_sah(B, m.tri_off);
+    // SRR_BVH_OPT: 0 = binned SAH + greedy collapse (round 3), 1 = + treelet
+    // restructuring + SAH-optimal collapse (default)
+    static const int opt = [] {
+      const char* e = getenv("SRR_BVH_OPT");
+      return e ? atoi(e) : 1;
+    }();
+    std::vector<TNode> T = ref_topology ? tree_from_reference(B, m.tri_off) : tree_sah(B, m.tri_off);
+    const int root = 0;
+    if (!ref_topology && opt >= 1 && T.size() > 2) restructure(T, root, 3);
+    Collapse col(T);
     m.node4_off = (int)(F.node4.size() / 32);
+    double sah4 = 0;  // SAH cost of the 4-wide hierarchy built (SRR_BVH_STATS)
     std::function<int(int)> build = [&](int top) -> int {
       std::vector<int> kids{top};
-      while (kids.size() < 4) {  // open the largest inner node until 4 children
-        int best = -1;
-        float ba = -1.f;
-        for (size_t k = 0; k < kids.size(); ++k)
-          if (T[kids[k]].code < 0 && box_area(T[kids[k]].box) > ba) { ba = box_area(T[kids[k]].box); best = (int)k; }
-        if (best < 0) break;
-        const TNode n = T[kids[best]];
-        kids[best] = n.left;
-        kids.insert(kids.begin() + best + 1, n.right);
+      if (!ref_topology && opt >= 1 && T[top].code < 0) {
+        kids = col.children(top);
+      } else {
+        while (kids.size() < 4) {  // open the largest inner node until 4 children
+          int best = -1;
+          float ba = -1.f;
+          for (size_t k = 0; k < kids.size(); ++k)
+            if (T[kids[k]].code < 0 && box_area(T[kids[k]].box) > ba) { ba = box_area(T[kids[k]].box); best = (int)k; }
+          if (best < 0) break;
+          const TNode n = T[kids[best]];
+          kids[best] = n.left;
+          kids.insert(kids.begin() + best + 1, n.right);
+        }
       }
+      sah4 += kSahNode4 * box_area(T[top].box);
+      for (int k : kids)
+        if (T[k].code >= 0) sah4 += kSahTri * leaf_tris(T[k]) * box_area(T[k].box);
       const int me = (int)(F.node4.size() / 32);
       F.node4.resize(F.node4.size() + 32);
       int32_t child[4] = {INT32_MIN, INT32_MIN, INT32_MIN, INT32_MIN};  // empty: never descended
@@ -793,8 +976,11 @@ struct Flattener {
       std::memcpy(d + 24, child, 16);
       return me;
     };
-    build(0);
+    build(root);
     m.n_node4 = (int)(F.node4.size() / 32) - m.node4_off;
+    if (getenv("SRR_BVH_STATS"))
+      fprintf(stderr, "srr bvh4: %d leaf units, %d nodes, SAH cost %.4f (x root area)\n", (int)(T.size() + 1) / 2,
+              m.n_node4, sah4 / std::max(1e-30, (double)box_area(T[root].box)));
     // breadth-first layout: the top levels come first, so the path kernel can
     // keep a prefix of the array in LDS (SceneView::node4_lds)
     std::vector<int> order{m.node4_off}, newidx(F.node4.size() / 32, -1);
