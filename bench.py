@@ -360,6 +360,7 @@ def main():
                 if j.get("world_rays_per_launch"):
                     cj, cnt = j, f
                     break
+        cnt_round = os.path.basename(os.path.dirname(cnt)) if cnt else ""
         if cj is not None and trace_ms > 0 and rays > 0:
             insts_per_ray = cj["raw_per_launch"]["SQ_INSTS_VALU"] / cj["world_rays_per_launch"]
             clock = cj.get("clock_ghz") or 2.4
@@ -375,7 +376,9 @@ def main():
                           f"{cj.get('profiled_workload', '?')})"}
             ws = cj.get("wave_time_split") or {}
             hbm = cj.get("hbm") or {}
-            if traffic is None and hbm.get("total_bytes"):
+            # the counter summary's HBM bytes (FETCH_SIZE / WRITE_SIZE passes of the same
+            # profiling run) take precedence over an older separate traffic summary
+            if hbm.get("total_bytes") and (traffic is None or cnt_round >= "r04"):
                 # measured HBM bytes per world ray of the profiled frame, priced on this run's launches
                 traffic = round(hbm["total_bytes"] / cj["world_rays_per_launch"] * rays / max(launches, 1))
                 out["roofline"]["traffic"] = traffic
