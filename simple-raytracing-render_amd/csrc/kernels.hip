@@ -1560,8 +1560,14 @@ SRR_D V3 random_in_unit_sphere(Rng& rng) {
   return p;
 }
 
-// light list (hitable_pdf over a hitable_list, hitable_list.h:54-67)
-__device__ __noinline__ float light_pdf_other(const SceneView& S, const DLight& L, V3 o, V3 v);
+// light list (hitable_pdf over a hitable_list, hitable_list.h:54-67).  The sphere /
+// triangle lights are out-of-line calls (rare kinds; inlined they bloat every
+// variant), taking their tables, the light and the RNG state BY VALUE: a
+// reference to the scene view or the Rng would give the caller's copies an
+// address, and the path kernel would then keep them in scratch memory -- every
+// RNG draw a scratch store (round 3's ALLFAM / MEDIA variants did).
+__device__ __noinline__ float light_pdf_other(const DSphere* spheres, const DStandaloneTri* stris, DLight L, V3 o,
+                                              V3 v);
 
 SRR_D float light_pdf_one(const SceneView& S, const DLight& L, V3 o, V3 v) {
   Ray r{o, v, 0.0f};
@@ -1577,13 +1583,14 @@ SRR_D float light_pdf_one(const SceneView& S, const DLight& L, V3 o, V3 v) {
     return 0;
   }
   if (L.kind == LIGHT_NONE) return 0.0;
-  return light_pdf_other(S, L, o, v);
+  return light_pdf_other(S.spheres, S.stris, L, o, v);
 }
 
-__device__ __noinline__ float light_pdf_other(const SceneView& S, const DLight& L, V3 o, V3 v) {
+__device__ __noinline__ float light_pdf_other(const DSphere* spheres, const DStandaloneTri* stris, DLight L, V3 o,
+                                              V3 v) {
   Ray r{o, v, 0.0f};
   if (L.kind == LIGHT_SPHERE) {  // sphere.h:69-78
-    const DSphere& s = S.spheres[L.idx];
+    const DSphere& s = spheres[L.idx];
     float t;
     if (sphere_hit(s, false, r, 0.001f, FLT_MAX, t)) {
       V3 c = v3(s.c0[0], s.c0[1], s.c0[2]);
@@ -1594,7 +1601,7 @@ __device__ __noinline__ float light_pdf_other(const SceneView& S, const DLight& 
     return 0;
   }
   if (L.kind == LIGHT_TRI) {  // triangle.h:70-87
-    const DStandaloneTri& T = S.stris[L.idx];
+    const DStandaloneTri& T = stris[L.idx];
     V3 p0 = v3(T.p[0], T.p[1], T.p[2]), p1 = v3(T.p[3], T.p[4], T.p[5]), p2 = v3(T.p[6], T.p[7], T.p[8]);
     float t, u, vv;
     if (tri_hit(p0, p1, p2, true, o, v / length(v), t, u, vv)) {
@@ -1626,7 +1633,12 @@ SRR_D float lights_pdf(const SceneView& S, V3 o, V3 v) {
   return sum;
 }
 
-__device__ __noinline__ V3 light_random_other(const SceneView& S, const DLight& L, V3 o, Rng& rng);
+struct LightDraw {  // light_random_other's direction and the LCG state after its draws
+  V3 d;
+  uint64_t lcg;
+};
+__device__ __noinline__ LightDraw light_random_other(const DSphere* spheres, const DStandaloneTri* stris, DLight L,
+                                                     V3 o, uint64_t lcg);
 
 // one light's random() (aarect.h:57-60, sphere.h:80-86, triangle.h:89-94)
 SRR_D V3 light_random_one(const SceneView& S, const DLight& L, V3 o, Rng& rng) {
@@ -1637,7 +1649,9 @@ SRR_D V3 light_random_one(const SceneView& S, const DLight& L, V3 o, Rng& rng) {
     return v3(x, q.k, z) - o;
   }
   if (L.kind == LIGHT_NONE) return v3(1, 0, 0);
-  return light_random_other(S, L, o, rng);
+  const LightDraw ld = light_random_other(S.spheres, S.stris, L, o, rng.lcg);
+  rng.lcg = ld.lcg;
+  return ld.d;
 }
 
 // hitable_list::random over the light list (hitable_list.h:63-67)
@@ -1646,9 +1660,11 @@ SRR_D V3 lights_random(const SceneView& S, V3 o, Rng& rng) {
   return light_random_one(S, S.lights[index], o, rng);
 }
 
-__device__ __noinline__ V3 light_random_other(const SceneView& S, const DLight& L, V3 o, Rng& rng) {
+__device__ __noinline__ LightDraw light_random_other(const DSphere* spheres, const DStandaloneTri* stris, DLight L,
+                                                     V3 o, uint64_t lcg) {
+  Rng rng{lcg, 0};  // (drand48 draws only: the PCG stream is not used here)
   if (L.kind == LIGHT_SPHERE) {  // sphere.h:7-15, 80-86
-    const DSphere& s = S.spheres[L.idx];
+    const DSphere& s = spheres[L.idx];
     V3 dirc = v3(s.c0[0], s.c0[1], s.c0[2]) - o;
     float d2 = squared_length(dirc);
     Onb uvw = onb_from_w(dirc);
@@ -1658,16 +1674,16 @@ __device__ __noinline__ V3 light_random_other(const SceneView& S, const DLight& 
     float phi = 2 * kPi * r1;
     float x = rcos(phi) * rsqrt_exact(1 - z * z);
     float y = rsin(phi) * rsqrt_exact(1 - z * z);
-    return onb_local(uvw, v3(x, y, z));
+    return LightDraw{onb_local(uvw, v3(x, y, z)), rng.lcg};
   }
   if (L.kind == LIGHT_TRI) {  // triangle.h:89-94
-    const DStandaloneTri& T = S.stris[L.idx];
+    const DStandaloneTri& T = stris[L.idx];
     float u = drand(rng);
     float v = drand(rng) * (1 - u);
     V3 p0 = v3(T.p[0], T.p[1], T.p[2]), p1 = v3(T.p[3], T.p[4], T.p[5]), p2 = v3(T.p[6], T.p[7], T.p[8]);
-    return p0 * (1 - u - v) + p1 * u + p2 * v - o;
+    return LightDraw{p0 * (1 - u - v) + p1 * u + p2 * v - o, rng.lcg};
   }
-  return v3(1, 0, 0);
+  return LightDraw{v3(1, 0, 0), rng.lcg};
 }
 
 // The BSDF half of the mixture (pdf.h:30-156) for one non-specular hit.
