@@ -10,8 +10,11 @@ case "$1" in
   counters)
     # the frames are cut to 256 spp where a full one takes seconds: counters.py records the
     # profiled frame's world rays, and bench.py prices the counts per world ray
+    shift
+    want=" $* "  # optional subset of config tags
     while read -r tag args; do
       [ -z "$tag" ] && continue
+      [ "$want" != "  " ] && [[ "$want" != *" $tag "* ]] && continue
       bash tools/counters.sh r04cnt_$tag $args > $O/r04cnt_$tag.log 2>&1 || { echo "counters $tag failed"; tail -5 $O/r04cnt_$tag.log; exit 1; }
       echo "$tag: $(python -c "import json; d=json.load(open('$O/r04cnt_$tag.json')); print(d['ms_per_launch_profiled'], 'ms', d.get('valu_lane_utilisation'), 'lanes', d['hbm']['total_bytes'], 'B', d['world_rays_per_launch'], 'rays')")"
     done <<'CFG'
