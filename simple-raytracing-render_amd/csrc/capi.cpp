@@ -388,6 +388,9 @@ int srr_render_device(srr_renderer* r, const srr_params* p, float* d_mean, srr_s
     pix.resize(npix);
     srr_shard_pixels(p, pix.data());
   }
+  // a new list overwrites the held one before anything can fail: forget its key
+  // until the render succeeds (a failed call must not leave the old shard "held")
+  if (!held) r->pix_key[0] = -1;
   std::string err;
   int rc = render_device(r, p, held ? nullptr : pix.data(), npix, d_mean, stats, err);
   if (rc < 0) return fail(rc, err);
@@ -412,6 +415,9 @@ int srr_render_device_async(srr_renderer* r, const srr_params* p, float* d_mean,
     pix.resize(npix);
     srr_shard_pixels(p, pix.data());
   }
+  // a new list overwrites the held one before anything can fail: forget its key
+  // until the render succeeds (a failed call must not leave the old shard "held")
+  if (!held) r->pix_key[0] = -1;
   std::string err;
   int rc = render_device_async(r, p, held ? nullptr : pix.data(), npix, d_mean, ticket, err);
   if (rc < 0) return fail(rc, err);
