@@ -1731,8 +1731,13 @@ template <bool BECK>
 SRR_D void bsdf_prepare(Bsdf& f, V3 wo) {
   if (BECK) return;
   f.flip = dot(-wo, f.n) > 0;
-  if (f.kind == MAT_LAMBERTIAN) f.co = dot(unit_vector(wo), f.n);
-  else f.lo = to_local_unit(f.uvw, -wo);
+  // (both fields written on every path: one of them left unset kept f in scratch)
+  float co = 0;
+  V3 lo = v3(0.f);
+  if (f.kind == MAT_LAMBERTIAN) co = dot(unit_vector(wo), f.n);
+  else lo = to_local_unit(f.uvw, -wo);
+  f.co = co;
+  f.lo = lo;
 }
 
 template <bool BECK>
@@ -1839,7 +1844,14 @@ struct DiffSetup {
 
 SRR_D DiffSetup diff_setup(const Bsdf& f, V3 p) {
   const bool on = f.kind != MAT_LAMBERTIAN;
-  return DiffSetup{p, f.uvw.w, f.uvw.v, on ? f.lo : f.n, on ? f.A : f.co, f.B, (on ? 1 : 0) | (f.flip ? 2 : 0)};
+  // (selected as values, not as one of two addresses in f)
+  V3 nl = f.n;
+  float c0 = f.co;
+  if (on) {
+    nl = f.lo;
+    c0 = f.A;
+  }
+  return DiffSetup{p, f.uvw.w, f.uvw.v, nl, c0, f.B, (on ? 1 : 0) | (f.flip ? 2 : 0)};
 }
 
 SRR_D Bsdf bsdf_of(const DiffSetup& d) {
@@ -2058,11 +2070,12 @@ SRR_D bool bsdf_dead(const SceneView& S, const Bsdf& f, V3 p) {
       const float m = 1e-3f * (ps + fmaxf(fmaxf(fabsf(c.x), fabsf(c.y)), fabsf(c.z)) + r);
       if (!light_point_far(c, p, w, sgn, r + m)) return false;
     } else if (L.kind == LIGHT_TRI) {
-      const DStandaloneTri T = S.stris[L.idx];
+      const DStandaloneTri& T = S.stris[L.idx];  // (read in place: a copy indexed in a loop lived in scratch)
       float cs = 0;
 #pragma unroll
       for (int k2 = 0; k2 < 9; ++k2) cs = fmaxf(cs, fabsf(T.p[k2]));
       const float m = 1e-3f * (ps + cs);
+#pragma unroll
       for (int c = 0; c < 3; ++c)
         if (!light_point_far(v3(T.p[3 * c], T.p[3 * c + 1], T.p[3 * c + 2]), p, w, sgn, m)) return false;
     } else if (L.kind != LIGHT_NONE) {
