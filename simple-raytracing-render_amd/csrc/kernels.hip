@@ -2662,6 +2662,13 @@ __global__ void __launch_bounds__(BS, MINB) k_paths(PathsArgs A) {
   }
   __syncthreads();
   const int slot = blockIdx.x * blockDim.x + threadIdx.x;
+  // this lane's record column W.rec + slot, re-derived at each use: hoisted out of
+  // the loop as a 64-bit address it was live (and spilled) across every phase
+  const auto rec_at = [&](const PathWork& W, int k) -> float4* {
+    int s = slot;
+    asm volatile("" : "+v"(s));
+    return W.rec + ((size_t)k * W.lanes + s);
+  };
   int g = -1;  // path of this lane (a window numbers its paths below 2^31), -1 idle
   // the wave's unissued path indices [pool, pool_end): wave-uniform (scalar)
   uint32_t pool = 0, pool_end = 0;
@@ -2884,7 +2891,7 @@ __global__ void __launch_bounds__(BS, MINB) k_paths(PathsArgs A) {
           else if (fam == FAM_BECK) scatter<FAM_BECK>(S, M, r.d, r.tm, h.p, h.n, h.u, h.v, rng, rec, sp, nd, nt);
           else scatter<FAM_SPEC>(S, M, r.d, r.tm, h.p, h.n, h.u, h.v, rng, rec, sp, nd, nt);
           if (depth >= W.max_depth || slot >= W.lanes) atomicOr(W.err, 2);
-          else rec_store(&W.rec[(size_t)depth * W.lanes + slot], rec);
+          else rec_store(rec_at(W, depth), rec);
           if (!sp && S.n_lights > 0 && rec.w == 0) ++n_capped;  // the loop reached kMixtureGuard
           r = Ray{h.p, nd, nt};
           ++depth;
@@ -2917,7 +2924,7 @@ __global__ void __launch_bounds__(BS, MINB) k_paths(PathsArgs A) {
       if (c < 0) c = 0;
       const V3 as = d_atten * (c / kPi);
       if (depth >= W.max_depth || slot >= W.lanes) atomicOr(W.err, 2);
-      else rec_store(&W.rec[(size_t)depth * W.lanes + slot], make_float4(as.x, as.y, as.z, d_pdf));
+      else rec_store(rec_at(W, depth), make_float4(as.x, as.y, as.z, d_pdf));
       r = Ray{ds.p, d_dir, r.tm};
       ++depth;
     }
@@ -2936,7 +2943,7 @@ __global__ void __launch_bounds__(BS, MINB) k_paths(PathsArgs A) {
       if (done) {
         // fold the bounces back to front (Raytracing_n.cpp:69, :94), as finish_path
         for (int k = depth - 1; k >= 0; --k) {
-          const float4 a = rec_load(&W.rec[(size_t)k * W.lanes + slot]);
+          const float4 a = rec_load(rec_at(W, k));
           const V3 av = v3(a.x, a.y, a.z);
           if (__float_as_uint(a.w) == kSpecMark) C = av * C;  // specular: attenuation * color
           else C = v3(0.f) + (av * C) / a.w;
