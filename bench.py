@@ -136,7 +136,8 @@ def cpu_baseline_reference(text, nx, ny, spp, max_depth, budget_s):
 
         def run(p0, stride):
             return subprocess.Popen([harness, "sums", scene, str(nx), str(ny), str(spp), str(max_depth), str(p0),
-                                     str(npix), "-", str(stride)], stdout=subprocess.PIPE, text=True)
+                                     str(npix), "-", str(stride)], stdout=subprocess.PIPE, text=True,
+                                    cwd=td)  # the reference opens its static outfile relative to the cwd (:45)
 
         # calibrate (and warm every core up: a cold first burst of processes runs
         # several times slower): each process ~32 pixels spread over the frame

@@ -1,3 +1,15 @@
+// SPDX-License-Identifier: LGPL-2.1-or-later
+// Derived from the GNU C Library 2.35 (sysdeps/ieee754/dbl-64: s_sin.c, s_sincos.c,
+// e_asin.c, e_atan2.c, and their data tables) -- IBM Accurate Mathematical Library,
+// written by International Business Machines Corp.;
+// Copyright (C) 2001-2022 Free Software Foundation, Inc.
+// The GNU C Library is free software; you can redistribute it and/or modify it
+// under the terms of the GNU Lesser General Public License as published by the
+// Free Software Foundation; either version 2.1 of the License, or (at your
+// option) any later version.  It is distributed WITHOUT ANY WARRANTY; see the
+// GNU Lesser General Public License (<https://www.gnu.org/licenses/>) for details.
+// Provenance of every third-party-derived file: THIRD_PARTY_NOTICES.md.
+//
 // The reference's double-precision libm calls of the MERL lookup (brdf.h:106-151:
 // cos, sin, acos, atan2), rounded exactly as on its host.
 //

@@ -2,10 +2,15 @@
 // table index of an (in, out) direction pair in half/difference-angle
 // coordinates (Rusinkiewicz), and the scaled RGB value stored there.  Host and
 // device share this code; every operation is double precision in the
-// reference's order (kernels are built with -ffp-contract=off), and the
-// reference's double cos / sin / acos / atan2 are glibc's own algorithms
-// (glibc_math64.h), so the cell of every query -- out == in included, where
-// phi_diff is atan2 of ~1e-17 residues -- is the reference's.
+// reference's order (kernels are built with -ffp-contract=off), and its double
+// cos / sin / acos / atan2 are glibc 2.35's own algorithms (glibc_math64.h), so
+// the cell of every query -- out == in included, where phi_diff is atan2 of
+// ~1e-17 residues -- is the one the ORACLE PORT computes: the reference's
+// brdf.h compiled here by g++ -O2 against glibc 2.35 on an FMA-capable x86-64
+// (oracle/ref).  The reference itself is an MSVC v142 project
+// (Raytracing_n.vcxproj) whose UCRT libm is a different implementation: for
+// out == in, parity with that build is unpinned; other queries can
+// differ only where an angle lies within a few ulps of a cell boundary.
 //
 // Reference: brdf.h:7-15 (resolution, channel scales), :17-61 (index
 // functions), :70-154 (vector helpers, std_coords_to_half_diff_coords),
@@ -79,7 +84,7 @@ SRR_HD void rotate(const double* v, const double* axis, double angle, double* ou
 // difference vector from the normalised incoming one.
 SRR_HD void half_diff(double theta_in, double fi_in, double theta_out, double fi_out, double& theta_half,
                       double& fi_half, double& theta_diff, double& fi_diff) {
-  // (the reference's g++ -O2 build merges each of the four angles' sin and cos
+  // (the oracle port's g++ -O2 build merges each of the four angles' sin and cos
   // into one glibc sincos() call -- a different, non-FMA build of the algorithm --
   // while rotate()'s cos / sin stay separate calls)
   double ip, iz, sfi, cfi;

@@ -1,3 +1,18 @@
+// SPDX-License-Identifier: LGPL-2.1-or-later
+// Derived from the GNU C Library 2.35 float math (sysdeps/ieee754/flt-32: e_expf.c,
+// e_logf.c, e_powf.c, s_sinf.c, s_cosf.c and their data tables, contributed by
+// Arm Ltd., Copyright (c) 2017-2018 Arm Ltd.; e_acosf.c, e_asinf.c, s_atanf.c,
+// e_atan2f.c from fdlibm, Copyright (C) 1993 by Sun Microsystems, Inc. -- "Developed
+// at SunPro, a Sun Microsystems, Inc. business.  Permission to use, copy, modify,
+// and distribute this software is freely granted, provided that this notice is
+// preserved.").  Copyright (C) 1991-2022 Free Software Foundation, Inc.
+// The GNU C Library is free software; you can redistribute it and/or modify it
+// under the terms of the GNU Lesser General Public License as published by the
+// Free Software Foundation; either version 2.1 of the License, or (at your
+// option) any later version.  It is distributed WITHOUT ANY WARRANTY; see the
+// GNU Lesser General Public License (<https://www.gnu.org/licenses/>) for details.
+// Provenance of every third-party-derived file: THIRD_PARTY_NOTICES.md.
+//
 // The reference's float libm calls, rounded exactly as on its host.
 //
 // The reference calls expf, logf, powf, sinf, cosf and acosf (via <cmath>'s float

@@ -45,6 +45,28 @@ KATS = [("erf", 512), ("beckmann11", 512), ("beckmann_dist", 512), ("beckmann_pd
         ("camera", 256), ("lights", 256), ("light_list", 256), ("merl", 2048), ("merl_same", 4096)]
 
 
+# The MERL KATs' out == in records are decided by the last-ulp rounding of glibc's
+# dbl-64 sin / cos / sincos / acos / atan2 (include/srr/merl.h): they are pinned to
+# the oracle port as built on glibc 2.35 with the FMA ifunc variants (__sin_fma,
+# __cos_fma, __ieee754_acos_fma, __ieee754_atan2_fma), which the device restates.
+# Another glibc, or a CPU without FMA (the ifunc then picks the SSE2 builds), gives
+# other cells; such a host must not regenerate them.
+MERL_LIBM_PIN = {"glibc": "glibc 2.35", "fma_ifunc": True}
+MERL_KATS = ("merl", "merl_same")
+
+
+def host_libm():
+    """The glibc version and whether its ifunc resolvers select the FMA variants
+    (glibc picks them when the CPU has FMA and AVX2)."""
+    flags = set()
+    with open("/proc/cpuinfo") as f:
+        for line in f:
+            if line.startswith("flags"):
+                flags = set(line.split(":", 1)[1].split())
+                break
+    return {"glibc": os.confstr("CS_GNU_LIBC_VERSION"), "fma_ifunc": "fma" in flags and "avx2" in flags}
+
+
 def run(*args):
     out = subprocess.run([HARNESS, *map(str, args)], check=True, capture_output=True, text=True)
     return out.stdout
@@ -53,7 +75,8 @@ def run(*args):
 def main():
     if not os.path.exists(HARNESS):
         sys.exit("build the reference harness first: make -C oracle ref")
-    meta = {"renders": {}, "kats": {}}
+    libm = host_libm()
+    meta = {"renders": {}, "kats": {}, "merl_libm": MERL_LIBM_PIN}
     for name, fac, nx, ny, spp, md in RENDERS:
         txt = os.path.join(HERE, f"{name}.scene")
         with open(txt, "w") as f:
@@ -63,6 +86,10 @@ def main():
         meta["renders"][name] = dict(nx=nx, ny=ny, spp=spp, max_depth=md, world_rays=stats["world_rays"])
         print(name, stats)
     for name, n in KATS:
+        if name in MERL_KATS and libm != MERL_LIBM_PIN:
+            print(f"kat_{name}.bin NOT regenerated: this host's libm {libm} is not the pinned {MERL_LIBM_PIN}")
+            meta["kats"][name] = n
+            continue
         run("kat", name, n, 1234567, os.path.join(HERE, f"kat_{name}.bin"))
         meta["kats"][name] = n
     run("teapot", 60.0, 10, os.path.join(HERE, "teapot_s60_d10.f32"))

@@ -1,8 +1,11 @@
 """MERL measured-BRDF lookup (brdf.h): the product's lookup
 (include/srr/merl.h through srr_merl_* on the device, and the same header built
-for the host) against the REFERENCE's own std_coords_to_half_diff_coords +
-lookup_brdf_val on a synthetic 90x90x180x3 table (the measured .binary files are
-not shipped with the reference):
+for the host) against the reference's own std_coords_to_half_diff_coords +
+lookup_brdf_val as compiled HERE (oracle/ref: g++ -O2, glibc 2.35, FMA ifunc
+variants; the reference ships as an MSVC project whose UCRT libm is another
+implementation, so for out == in the pin is to this oracle port and parity with
+the MSVC build is unpinned) on a synthetic 90x90x180x3 table (the measured
+.binary files are not shipped with the reference):
 
 * tests/golden/kat_merl.bin: random (in, out) angle pairs, every 5th with
   out == in, every 7th with theta_in = 0 (oracle/ref kat.inc "merl");
@@ -63,6 +66,14 @@ def test_kat_shapes():
     assert deg1.sum() >= len(deg1) // 6 and (~deg1).sum() > len(deg1) // 2
     assert deg2.all() and len(deg2) == 4096
     assert len(np.unique(c2 % 180)) > 20
+
+
+def test_merl_kats_record_their_libm():
+    """The KATs' libm is recorded (tests/golden/make_golden.py refuses to
+    regenerate them on another glibc or without the FMA ifunc variants)."""
+    import json
+    meta = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))
+    assert meta["merl_libm"] == {"glibc": "glibc 2.35", "fma_ifunc": True}
 
 
 def test_merl_host_build_matches_reference(tmp_path):

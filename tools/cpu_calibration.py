@@ -27,7 +27,8 @@ def ref_rate(scene, nx, ny, spp, step, procs):
     npix = nx * ny
     t0 = time.perf_counter()
     ps = [subprocess.Popen([h, "sums", scene, str(nx), str(ny), str(spp), "50", str(k * step), str(npix), "-",
-                            str(procs * step)], stdout=subprocess.PIPE, text=True) for k in range(procs)]
+                            str(procs * step)], stdout=subprocess.PIPE, text=True, cwd=os.path.dirname(scene))
+          for k in range(procs)]
     outs = [json.loads(p.communicate()[0].strip().splitlines()[-1]) for p in ps]
     dt = time.perf_counter() - t0
     rays = sum(o["world_rays"] for o in outs)
