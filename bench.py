@@ -68,6 +68,14 @@ def parse():
                     help="take the multi-rank code path even at world size 1 (init_process_group over "
                          "SRR_DIST_BACKEND, the frame-end gather/reduce through the collective): run under "
                          "torch.distributed.run --nproc-per-node 1 it executes the RCCL leg on one GPU")
+    ap.add_argument("--host", default="torch", choices=["torch", "capi"],
+                    help="torch: one process per GPU, the frame-end gather over torch.distributed (the driver's "
+                         "torch.distributed.run launch); capi: ONE process drives --gpus N devices through the C-ABI "
+                         "(srr_renderer_create_multi: a host thread or async frame per device, one RCCL "
+                         "ncclSend/ncclRecv gather to device 0 from C++), run without torch.distributed.run")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="--host capi on fewer GPUs than --gpus: the N shards share the visible devices (gather by "
+                         "device copies instead of RCCL); for correctness rehearsals, not a scaling number")
     ap.add_argument("--save-frame", default="",
                     help="rank 0 saves the assembled frame of the last step (per-pixel means, .npy)")
     return ap.parse_args()
@@ -159,6 +167,178 @@ def cpu_baseline_reference(text, nx, ny, spp, max_depth, budget_s):
                       f"one single-threaded process per core"}
 
 
+def bench_line(a, text, cfg, nx, ny, spp, rays_total, elapsed, trace_ms, launches, world, workload_tail,
+               parallelism, extra, rays_local=None, frame_spp=None, visits=None):
+    """The JSON line (rank 0): value = every device's world rays over the slowest
+    rank's time; the roofline prices rank 0's own rays (rays_local; all of them
+    for --host capi, whose trace_ms / launches sum every device's) over its
+    kernel time."""
+    launches_total = launches
+    rays = rays_total if rays_local is None else rays_local
+    counts_json = json.load(open(os.path.join(ROOT, "tests", "golden", "traversal_counts.json")))
+    key = CONFIG_KEY[a.scene]
+    default_divs = {"s2": 10, "s3": 10, "s3_metal": 10, "s4": 40, "s5": 40}.get(a.scene)
+    if a.divs and a.divs != default_divs:
+        key = f"{key}_d{a.divs}"
+    if key not in counts_json:
+        raise SystemExit(f"no reference traversal counts for {key}: add it to tests/golden/make_counts.py")
+    b_cfg = counts_json[key]["B_cfg"]
+    value = rays_total / elapsed / 1e6
+    # roofline of the dominant kernel (srr_trace) on rank 0: algorithmic bytes
+    # (B_cfg per world ray, reference traversal counts) over its HIP-event time
+    achieved = rays * b_cfg / (trace_ms * 1e-3) / 1e9 if trace_ms > 0 else None
+    wave = bool(os.environ.get("SRR_ENGINE") == "wave")
+    kernel_name = ("k_trace (wavefront engine)" if wave else
+                   "k_paths (path-resident persistent kernel: trace + shade)")
+    traffic = None
+    # measured HBM bytes of k_paths (tools/pmc_traffic.py).  A summary that records its
+    # frame's world rays is priced per world ray on this run's launches; an older one only
+    # stands for the default single-GPU frame it was measured on
+    pmc = os.path.join(ROOT, "profiles", f"pmc_{a.scene}{key[len(CONFIG_KEY[a.scene]):]}.json")
+    default_frame = (world == 1 and a.plan == "tiles" and (nx, ny, spp) == (cfg["nx"], cfg["ny"], cfg["spp"]))
+    if os.path.exists(pmc) and launches:
+        pj = json.load(open(pmc))
+        if pj.get("kernel", "") in kernel_name:
+            if pj.get("world_rays_per_launch"):
+                traffic = round(pj["hbm_bytes_per_launch"] / pj["world_rays_per_launch"] * rays / launches)
+            elif default_frame:
+                traffic = pj.get("hbm_bytes_per_launch")
+    out = {
+        "metric": "Msamples/s (rays x bounces) + HBM GB/s vs roofline, Cornell+teapot 1024spp",
+        "value": round(value, 3),
+        "unit": "Msamples/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak" if a.plan == "samples" else "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": ("the reference's own assets (Soilder.FBX mesh 0, sky4.jpg, textures) via the committed fixture"
+                 if a.scene == "s4_real" else
+                 "synthetic (scene built in code: Cornell box + tessellated Utah teapot)"),
+        "config": dict({"workload": f"{key}: {a.scene}{f' divs {a.divs}' if a.divs else ''} {nx}x{ny} {spp}spp "
+                                    f"maxDepth {cfg['max_depth']}" + workload_tail,
+                        "nx": nx, "ny": ny, "spp_per_gpu" if a.plan == "samples" else "spp": spp,
+                        "frame_spp": frame_spp or spp, "world_rays_per_step": int(rays_total / a.steps),
+                        "parallelism": parallelism}, **extra),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                     "traffic": traffic, "kernel": kernel_name, "B_cfg": round(b_cfg, 1),
+                     "trace_ms_per_launch": round(trace_ms / max(launches, 1), 4),
+                     "trace_launches": launches_total,
+                     "basis": "achieved/frac count ALGORITHMIC bytes: B_cfg per world ray from the "
+                              "reference's traversal counts (SURVEY 8(d)); traffic is the measured HBM bytes",
+                     "traffic_GBps": (round(traffic / (trace_ms / max(launches, 1) * 1e-3) / 1e9, 1)
+                                      if traffic and trace_ms > 0 else None),
+                     "measured_bound": "issue/latency: the scene lives in LDS and L2 (no counter summary of "
+                                       "this config in profiles/)"},
+    }
+    # issue roofline of the same kernel from a committed PMC summary (tools/counters.sh ->
+    # profiles/rNN/counters_<scene>.json, newest round first): VALU wave-instructions per
+    # world ray of the profiled frame, times the world rays rank 0 traced here, over rank 0's
+    # live kernel time -- so a shard, another frame size or another spp is priced by its own
+    # rays, not by the profiled frame's -- against 1,024 SIMDs each issuing one wave64 VALU
+    # instruction per 2 cycles (SIMD-32, MI355X_MICROARCH.md)
+    cj, cnt = None, None
+    suffix = key[len(CONFIG_KEY[a.scene]):]
+    for rdir in sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]")), reverse=True):
+        f = os.path.join(rdir, f"counters_{a.scene}{suffix}.json")
+        if os.path.exists(f):
+            j = json.load(open(f))
+            if j.get("world_rays_per_launch"):
+                cj, cnt = j, f
+                break
+    cnt_round = os.path.basename(os.path.dirname(cnt)) if cnt else ""
+    if cj is not None and trace_ms > 0 and rays > 0:
+        insts_per_ray = cj["raw_per_launch"]["SQ_INSTS_VALU"] / cj["world_rays_per_launch"]
+        clock = cj.get("clock_ghz") or 2.4
+        rate = insts_per_ray * rays / (trace_ms * 1e-3)
+        peak = 1024 * clock * 1e9 / 2
+        lane = cj.get("valu_lane_utilisation")
+        out["roofline"]["issue"] = {
+            "valu_wave_insts_per_s": round(rate, -6), "peak": round(peak, -6), "frac": round(rate / peak, 4),
+            "lane_utilisation": lane, "lane_frac": round(rate / peak * lane, 4) if lane else None,
+            "valu_wave_insts_per_world_ray": round(insts_per_ray, 3),
+            "wave_time_split": cj.get("wave_time_split"), "clock_ghz": clock,
+            "source": os.path.relpath(cnt, ROOT) + f" ({cj.get('ms_per_launch_profiled')} ms/launch profiled, "
+                      f"{cj.get('profiled_workload', '?')})"}
+        ws = cj.get("wave_time_split") or {}
+        hbm = cj.get("hbm") or {}
+        # the counter summary's HBM bytes (FETCH_SIZE / WRITE_SIZE passes of the same
+        # profiling run) take precedence over an older separate traffic summary
+        if hbm.get("total_bytes") and (traffic is None or cnt_round >= "r04"):
+            # measured HBM bytes per world ray of the profiled frame, priced on this run's launches
+            traffic = round(hbm["total_bytes"] / cj["world_rays_per_launch"] * rays / max(launches, 1))
+            out["roofline"]["traffic"] = traffic
+            out["roofline"]["traffic_GBps"] = round(traffic / (trace_ms / max(launches, 1) * 1e-3) / 1e9, 1)
+        out["roofline"]["measured_bound"] = (
+            f"latency/issue: VALU pipe {100 * rate / peak:.0f}% busy at {100 * (lane or 0):.0f}% lane "
+            f"utilisation, waves {100 * ws.get('waiting_on_memory_or_barrier', 0):.0f}% of their time waiting; "
+            f"HBM {100 * (out['roofline']['traffic_GBps'] or 0) / HBM_PEAK_GBS:.1f}% of peak")
+    if a.count_visits:
+        out["visits"] = {"box_tests_per_ray": visits[0] / max(rays, 1), "tri_tests_per_ray": visits[1] / max(rays, 1),
+                         "stack_overflows": visits[2], "note": "counting run: timing not representative"}
+    if world == 1 and not a.no_cpu_baseline:
+        # the reference's own code when its harness was built (oracle/_ref), else the
+        # bit-exact restatement; the two are different harnesses (processes vs threads),
+        # so neither calibrates the other (DESIGN §5)
+        ref = cpu_baseline_reference(text, nx, ny, spp, cfg["max_depth"], a.cpu_seconds)
+        out["cpu_baseline"] = ref if ref is not None else cpu_baseline(text, nx, ny, spp, a.cpu_seconds)
+    return out
+
+
+def bench_capi(a, rend, devices, text, sc, cfg, nx, ny, spp, dev, n_dev):
+    """--host capi: ONE process renders the whole frame over --gpus N devices
+    through srr_renderer_create_multi (C++: a host thread / async frame per device,
+    one RCCL gather of the shards' packed slabs to device 0, the scatter there).
+    A step is one whole assembled frame; two frames in flight unless
+    --no-pipeline."""
+    import torch
+
+    from srr import capi
+    p = capi.make_params(nx, ny, spp, cfg["max_depth"], tile=a.tile, batch_paths=a.batch_paths,
+                         flags=capi.FLAG_COUNT_VISITS if a.count_visits else 0)
+    pipeline = not (a.no_pipeline or a.count_visits)
+    bufs = [torch.zeros((nx * ny, 3), dtype=torch.float32, device=dev) for _ in range(2 if pipeline else 1)]
+
+    def run_frames(n):
+        if not pipeline:
+            return [rend.render_device(p, bufs[0].data_ptr()) for _ in range(n)]
+        stats, pend = [], []
+        for k in range(n):
+            pend.append(rend.render_device_async(p, bufs[k % 2].data_ptr()))
+            if len(pend) == 2:
+                stats.append(rend.wait(pend.pop(0)))
+        stats += [rend.wait(t) for t in pend]
+        return stats
+
+    run_frames(a.warmup)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    sts = run_frames(a.steps)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    rays = sum(st["world_rays"] for st in sts)
+    trace_ms = sum(st["trace_ms"] for st in sts)
+    launches = sum(st["trace_launches"] for st in sts)
+    visits = [sum(st[k] for st in sts) for k in ("box_tests", "tri_tests", "stack_overflows")]
+    if a.save_frame:
+        import numpy as np
+        np.save(a.save_frame, bufs[(a.steps - 1) % len(bufs)].cpu().numpy())
+    out = bench_line(a, text, cfg, nx, ny, spp, rays, elapsed, trace_ms, launches, world=a.gpus,
+                     workload_tail=(f", {a.tile}x{a.tile} tiles round-robin over {a.gpus} devices of ONE process "
+                                    f"(srr_renderer_create_multi), one {rend.transport.upper()} gather to device 0"
+                                    if a.gpus > 1 else f", whole frame on one GPU of ONE process "
+                                    f"(srr_renderer_create_multi), one {rend.transport.upper()} gather to device 0"),
+                     parallelism=f"tiles{a.gpus}", extra={"host": "capi", "devices": devices,
+                                                          "transport": rend.transport, "devices_seen": n_dev,
+                                                          "frames_in_flight": 2 if pipeline else 1},
+                     visits=visits)
+    print(json.dumps(out), flush=True)
+
+
 def main():
     a = parse()
     import torch
@@ -174,11 +354,16 @@ def main():
     # "gloo" (host-staged gather; lets several ranks share one GPU, e.g. the
     # 2-rank rehearsal of tests/test_bench_multirank.py on a one-GPU box)
     backend = os.environ.get("SRR_DIST_BACKEND", "nccl")
+    if a.host == "capi":
+        if world != 1:
+            raise SystemExit("--host capi is one process driving --gpus N devices: run it without torch.distributed.run")
+        if a.plan != "tiles":
+            raise SystemExit("--host capi renders the tiles plan (srr_renderer_create_multi)")
     if backend not in ("nccl", "gloo"):
         raise SystemExit(f"SRR_DIST_BACKEND must be nccl or gloo, not {backend!r}")
     n_dev = torch.cuda.device_count()  # counting devices does not initialise the GPU
     dev_idx = local % max(n_dev, 1)
-    use_dist = world > 1 or a.force_dist
+    use_dist = (world > 1 or a.force_dist) and a.host == "torch"
     if a.force_dist and "MASTER_ADDR" not in os.environ:
         raise SystemExit("--force-dist: run under torch.distributed.run (MASTER_ADDR/MASTER_PORT unset)")
     dist_world = 1
@@ -190,7 +375,10 @@ def main():
         dist_world = dist.get_world_size()
         if dist_world != world:
             raise SystemExit(f"communicator has {dist_world} ranks, WORLD_SIZE says {world}")
-    if a.gpus != world:
+    if a.host == "capi":
+        if n_dev < a.gpus and not a.rehearse:
+            raise SystemExit(f"--host capi --gpus {a.gpus}: {n_dev} GPUs visible (--rehearse shares them)")
+    elif a.gpus != world:
         raise SystemExit(f"--gpus {a.gpus} but {world} rank(s) were launched (use torch.distributed.run "
                          f"--nproc-per-node {a.gpus})")
     if backend == "nccl" and use_dist and n_dev < world:
@@ -210,6 +398,10 @@ def main():
     sc, cfg = fac()
     nx, ny, spp = a.nx or cfg["nx"], a.ny or cfg["ny"], a.spp or cfg["spp"]
     text = sc.text()
+    if a.host == "capi":
+        devices = [k % max(n_dev, 1) for k in range(a.gpus)]
+        rend = capi.Renderer(text, devices=devices)  # (at N = 1 too: an RCCL communicator of one device)
+        return bench_capi(a, rend, devices, text, sc, cfg, nx, ny, spp, dev, n_dev)
     rend = capi.Renderer(text, device=dev_idx)
     sh = dist_frame.plan_shard(nx, ny, spp, cfg["max_depth"], rank, world, plan=a.plan, tile=a.tile,
                                batch_paths=a.batch_paths, flags=capi.FLAG_COUNT_VISITS if a.count_visits else 0)
@@ -277,126 +469,16 @@ def main():
         np.save(a.save_frame, frame[0].cpu().numpy())
     if rank == 0:
         coll = "RCCL" if backend == "nccl" else "host-staged gloo"
-        launches_total = launches
-        counts_json = json.load(open(os.path.join(ROOT, "tests", "golden", "traversal_counts.json")))
-        key = CONFIG_KEY[a.scene]
-        default_divs = {"s2": 10, "s3": 10, "s3_metal": 10, "s4": 40, "s5": 40}.get(a.scene)
-        if a.divs and a.divs != default_divs:
-            key = f"{key}_d{a.divs}"
-        if key not in counts_json:
-            raise SystemExit(f"no reference traversal counts for {key}: add it to tests/golden/make_counts.py")
-        b_cfg = counts_json[key]["B_cfg"]
-        value = rays_total / elapsed / 1e6
-        # roofline of the dominant kernel (srr_trace) on rank 0: algorithmic bytes
-        # (B_cfg per world ray, reference traversal counts) over its HIP-event time
-        achieved = rays * b_cfg / (trace_ms * 1e-3) / 1e9 if trace_ms > 0 else None
-        wave = bool(os.environ.get("SRR_ENGINE") == "wave")
-        kernel_name = ("k_trace (wavefront engine)" if wave else
-                       "k_paths (path-resident persistent kernel: trace + shade)")
-        traffic = None
-        # measured HBM bytes of k_paths (tools/pmc_traffic.py).  A summary that records its
-        # frame's world rays is priced per world ray on this run's launches; an older one only
-        # stands for the default single-GPU frame it was measured on
-        pmc = os.path.join(ROOT, "profiles", f"pmc_{a.scene}{key[len(CONFIG_KEY[a.scene]):]}.json")
-        default_frame = (world == 1 and a.plan == "tiles" and (nx, ny, spp) == (cfg["nx"], cfg["ny"], cfg["spp"]))
-        if os.path.exists(pmc) and launches:
-            pj = json.load(open(pmc))
-            if pj.get("kernel", "") in kernel_name:
-                if pj.get("world_rays_per_launch"):
-                    traffic = round(pj["hbm_bytes_per_launch"] / pj["world_rays_per_launch"] * rays / launches)
-                elif default_frame:
-                    traffic = pj.get("hbm_bytes_per_launch")
-        out = {
-            "metric": "Msamples/s (rays x bounces) + HBM GB/s vs roofline, Cornell+teapot 1024spp",
-            "value": round(value, 3),
-            "unit": "Msamples/s",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(elapsed / a.steps * 1e3, 3),
-            "higher_is_better": True,
-            "scaling": "weak" if a.plan == "samples" else "strong",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": ("the reference's own assets (Soilder.FBX mesh 0, sky4.jpg, textures) via the committed fixture"
-                     if a.scene == "s4_real" else
-                     "synthetic (scene built in code: Cornell box + tessellated Utah teapot)"),
-            "config": {"workload": f"{key}: {a.scene}{f' divs {a.divs}' if a.divs else ''} {nx}x{ny} {spp}spp "
-                                   f"maxDepth {cfg['max_depth']}" + (
-                                   (f", {a.tile}x{a.tile} tiles round-robin over {world} GPUs, one {coll} gather "
-                                    f"to rank 0 at frame end" if use_dist else
-                                    ", whole frame on one GPU (no collective)")
-                                   if a.plan == "tiles" else
-                                   f" per GPU; {world} GPU(s) render sample ranges of one {spp * world}spp frame" +
-                                   (f", one {coll} reduce at frame end" if use_dist else "")),
-                       "nx": nx, "ny": ny, "spp_per_gpu" if a.plan == "samples" else "spp": spp,
-                       "frame_spp": sh.total_spp, "world_rays_per_step": int(rays_total / a.steps),
-                       "parallelism": f"{a.plan}{world}", "dist_backend": backend if use_dist else None,
-                       "dist_world": dist_world if use_dist else None, "devices_seen": n_dev,
-                       "frames_in_flight": 2 if pipeline else 1},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                         "traffic": traffic, "kernel": kernel_name, "B_cfg": round(b_cfg, 1),
-                         "trace_ms_per_launch": round(trace_ms / max(launches, 1), 4),
-                         "trace_launches": launches_total,
-                         "basis": "achieved/frac count ALGORITHMIC bytes: B_cfg per world ray from the "
-                                  "reference's traversal counts (SURVEY 8(d)); traffic is the measured HBM bytes",
-                         "traffic_GBps": (round(traffic / (trace_ms / max(launches, 1) * 1e-3) / 1e9, 1)
-                                          if traffic and trace_ms > 0 else None),
-                         "measured_bound": "issue/latency: the scene lives in LDS and L2 (no counter summary of "
-                                           "this config in profiles/)"},
-        }
-        # issue roofline of the same kernel from a committed PMC summary (tools/counters.sh ->
-        # profiles/rNN/counters_<scene>.json, newest round first): VALU wave-instructions per
-        # world ray of the profiled frame, times the world rays rank 0 traced here, over rank 0's
-        # live kernel time -- so a shard, another frame size or another spp is priced by its own
-        # rays, not by the profiled frame's -- against 1,024 SIMDs each issuing one wave64 VALU
-        # instruction per 2 cycles (SIMD-32, MI355X_MICROARCH.md)
-        cj, cnt = None, None
-        suffix = key[len(CONFIG_KEY[a.scene]):]
-        for rdir in sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]")), reverse=True):
-            f = os.path.join(rdir, f"counters_{a.scene}{suffix}.json")
-            if os.path.exists(f):
-                j = json.load(open(f))
-                if j.get("world_rays_per_launch"):
-                    cj, cnt = j, f
-                    break
-        cnt_round = os.path.basename(os.path.dirname(cnt)) if cnt else ""
-        if cj is not None and trace_ms > 0 and rays > 0:
-            insts_per_ray = cj["raw_per_launch"]["SQ_INSTS_VALU"] / cj["world_rays_per_launch"]
-            clock = cj.get("clock_ghz") or 2.4
-            rate = insts_per_ray * rays / (trace_ms * 1e-3)
-            peak = 1024 * clock * 1e9 / 2
-            lane = cj.get("valu_lane_utilisation")
-            out["roofline"]["issue"] = {
-                "valu_wave_insts_per_s": round(rate, -6), "peak": round(peak, -6), "frac": round(rate / peak, 4),
-                "lane_utilisation": lane, "lane_frac": round(rate / peak * lane, 4) if lane else None,
-                "valu_wave_insts_per_world_ray": round(insts_per_ray, 3),
-                "wave_time_split": cj.get("wave_time_split"), "clock_ghz": clock,
-                "source": os.path.relpath(cnt, ROOT) + f" ({cj.get('ms_per_launch_profiled')} ms/launch profiled, "
-                          f"{cj.get('profiled_workload', '?')})"}
-            ws = cj.get("wave_time_split") or {}
-            hbm = cj.get("hbm") or {}
-            # the counter summary's HBM bytes (FETCH_SIZE / WRITE_SIZE passes of the same
-            # profiling run) take precedence over an older separate traffic summary
-            if hbm.get("total_bytes") and (traffic is None or cnt_round >= "r04"):
-                # measured HBM bytes per world ray of the profiled frame, priced on this run's launches
-                traffic = round(hbm["total_bytes"] / cj["world_rays_per_launch"] * rays / max(launches, 1))
-                out["roofline"]["traffic"] = traffic
-                out["roofline"]["traffic_GBps"] = round(traffic / (trace_ms / max(launches, 1) * 1e-3) / 1e9, 1)
-            out["roofline"]["measured_bound"] = (
-                f"latency/issue: VALU pipe {100 * rate / peak:.0f}% busy at {100 * (lane or 0):.0f}% lane "
-                f"utilisation, waves {100 * ws.get('waiting_on_memory_or_barrier', 0):.0f}% of their time waiting; "
-                f"HBM {100 * (out['roofline']['traffic_GBps'] or 0) / HBM_PEAK_GBS:.1f}% of peak")
-        if a.count_visits:
-            out["visits"] = {"box_tests_per_ray": visits[0] / max(rays, 1), "tri_tests_per_ray": visits[1] / max(rays, 1),
-                             "stack_overflows": visits[2], "note": "counting run: timing not representative"}
-        if world == 1 and not a.no_cpu_baseline:
-            # the reference's own code when its harness was built (oracle/_ref), else the
-            # bit-exact restatement; the two are different harnesses (processes vs threads),
-            # so neither calibrates the other
-            ref = cpu_baseline_reference(text, nx, ny, spp, cfg["max_depth"], a.cpu_seconds)
-            out["cpu_baseline"] = ref if ref is not None else cpu_baseline(text, nx, ny, spp, a.cpu_seconds)
+        tail = ((f", {a.tile}x{a.tile} tiles round-robin over {world} GPUs, one {coll} gather to rank 0 at frame end"
+                 if use_dist else ", whole frame on one GPU (no collective)")
+                if a.plan == "tiles" else
+                f" per GPU; {world} GPU(s) render sample ranges of one {spp * world}spp frame" +
+                (f", one {coll} reduce at frame end" if use_dist else ""))
+        out = bench_line(a, text, cfg, nx, ny, spp, rays_total, elapsed, trace_ms, launches, world, tail,
+                         f"{a.plan}{world}", {"host": "torch", "dist_backend": backend if use_dist else None,
+                                              "dist_world": dist_world if use_dist else None, "devices_seen": n_dev,
+                                              "frames_in_flight": 2 if pipeline else 1},
+                         rays_local=rays, frame_spp=sh.total_spp, visits=visits)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -2,7 +2,8 @@
  * pick a scene builder by sceneid (:893-919), build it with the reference's
  * builder signature `void f(hitable** scene, camera** cam, hitable** hlist, float
  * aspect)` against include/srr/ref_api.h, render nx x ny x ns with maxDepth on
- * the GPU (the 8 render threads of :923-932 become one srr_render), print the
+ * the GPU(s) (the 8 render threads of :923-932 become one srr_render, over
+ * --gpus N devices of the node with one RCCL gather at frame end), print the
  * elapsed milliseconds (:934-937) and write the ASCII P3 image (:848-886).
  *
  *     int main(int argc, char** argv) {
@@ -16,6 +17,12 @@
  *                                (srr_scene_from_text), e.g. one of the reference's
  *                                builders written by python -m srr.ref_scenes
  *   --nx 1000 --ny 1000 --ns 50 --max-depth 50 --device 0 --out out.ppm
+ *   --gpus N                     render on devices device .. device+N-1
+ *                                (srr_renderer_create_multi: tiles of --tile
+ *                                pixels, default 1, dealt round-robin, one RCCL
+ *                                gather to the first device); bitwise the 1-GPU image
+ *   --devices 0,1,2,3            the same with an explicit device list (a list of
+ *                                one device still goes through the RCCL gather)
  *   --dry-run                    build the scene and print its digest
  *                                (srr_scene_digest), no GPU
  * Differences, all forced by the reference: its render threads race on shared
@@ -48,11 +55,14 @@ struct scene_entry {
 
 inline int render_main(int argc, char** argv, const scene_entry* scenes, int n_scenes) {
   int nx = 1000, ny = 1000, ns = 50, max_depth = 50, sceneid = 2, device = 0;  // Raytracing_n.cpp:39-43
+  int gpus = 1, tile = 1;
+  std::vector<int> devices;
   std::string name, out = "out.ppm", text_path;
   bool dry = false;
   auto usage = [&]() {
     std::fprintf(stderr, "usage: %s [--sceneid N | --scene NAME] [--nx N] [--ny N] [--ns N] [--max-depth N] "
-                         "[--device N] [--out FILE] [--dry-run]\nscenes:", argv[0]);
+                         "[--device N] [--gpus N | --devices a,b,..] [--tile N] [--out FILE] [--dry-run]\nscenes:",
+                 argv[0]);
     for (int k = 0; k < n_scenes; ++k) std::fprintf(stderr, " %d:%s", scenes[k].sceneid, scenes[k].name);
     std::fprintf(stderr, "\n");
     return 2;
@@ -73,6 +83,13 @@ inline int render_main(int argc, char** argv, const scene_entry* scenes, int n_s
     else if (a == "--ns") ok = num(ns);
     else if (a == "--max-depth") ok = num(max_depth);
     else if (a == "--device") ok = num(device);
+    else if (a == "--gpus") ok = num(gpus) && gpus >= 1;
+    else if (a == "--tile") ok = num(tile) && tile >= 1;
+    else if (a == "--devices" && i + 1 < argc) {
+      std::stringstream ds(argv[++i]);
+      for (std::string t; std::getline(ds, t, ',');) devices.push_back(std::atoi(t.c_str()));
+      ok = !devices.empty();
+    }
     else if (a == "--out" && i + 1 < argc) out = argv[++i];
     else if (a == "--dry-run") dry = true;
     else ok = false;
@@ -120,8 +137,13 @@ inline int render_main(int argc, char** argv, const scene_entry* scenes, int n_s
     srr_scene_destroy(s);
     return 0;
   }
+  const bool multi = !devices.empty() || gpus > 1;  // an explicit --devices list: multi even for one device
+  if (devices.empty())
+    for (int k = 0; k < gpus; ++k) devices.push_back(device + k);
   srr_renderer* r = nullptr;
-  if (srr_renderer_create(s, device, &r) < 0) {
+  const int rc0 = multi ? srr_renderer_create_multi(s, (int)devices.size(), devices.data(), &r)
+                        : srr_renderer_create(s, devices[0], &r);
+  if (rc0 < 0) {
     std::fprintf(stderr, "%s\n", srr_last_error());
     srr_scene_destroy(s);
     return 1;
@@ -131,7 +153,7 @@ inline int render_main(int argc, char** argv, const scene_entry* scenes, int n_s
   p.ny = ny;
   p.spp = ns;
   p.max_depth = max_depth;
-  p.tile = 1;
+  p.tile = tile;
   p.shard_count = 1;
   std::vector<unsigned char> rgb8(3 * (size_t)nx * ny);
   srr_stats st{};
@@ -142,8 +164,9 @@ inline int render_main(int argc, char** argv, const scene_entry* scenes, int n_s
   if (rc < 0) std::fprintf(stderr, "%s\n", srr_last_error());
   else {
     std::printf("%dms\n", (int)ms);  // :934-937
-    std::fprintf(stderr, "%s: %dx%dx%d, %lld world rays, %.1f Msamples/s -> %s\n", scene_name, nx, ny, ns,
-                 (long long)st.world_rays, st.world_rays / (ms * 1e3), out.c_str());
+    std::fprintf(stderr, "%s: %dx%dx%d, %lld world rays, %.1f Msamples/s on %d GPU(s) (%s) -> %s\n", scene_name, nx,
+                 ny, ns, (long long)st.world_rays, st.world_rays / (ms * 1e3), (int)devices.size(),
+                 srr_renderer_transport(r), out.c_str());
   }
   srr_renderer_destroy(r);
   srr_scene_destroy(s);

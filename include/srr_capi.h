@@ -189,6 +189,32 @@ typedef struct srr_stats {
 /* Flatten the scene and upload it to HIP device `device`. */
 int srr_renderer_create(const srr_scene* s, int device, srr_renderer** out);
 void srr_renderer_destroy(srr_renderer* r);
+/* One renderer over n_devices GPUs: the replacement for the
+ * reference's 8 renderthreads in one process (Raytracing_n.cpp:932-941) at node
+ * scale.  The scene is flattened once and uploaded to every device.  srr_render,
+ * srr_render_device, srr_render_device_async and srr_render_wait on the handle
+ * render the WHOLE frame (shard_index / shard_count must be 0 / 0 or 1): tiles of
+ * edge p->tile (<= 0: 32) dealt round-robin over the devices, each tile row
+ * rotated by one (srr_shard_pixels with shard_count = n_devices), all devices at
+ * once, then ONE frame-end gather of the packed shard slabs to device_ids[0] over
+ * RCCL (ncclCommInitAll communicator, ncclSend / ncclRecv in one group) and a
+ * scatter into the image there: d_mean is a device_ids[0] pointer of nx*ny*3
+ * floats, bitwise the one-device frame.  The calls return after the gather.
+ * device_ids may repeat a device (a rehearsal on one GPU): the gather is then
+ * device copies, as with SRR_MULTI_TRANSPORT=copy.  No KEEP_PATHS / CONTINUE
+ * (SRR_EINVAL); srr_accum_* and srr_copy_paths are single-device. */
+int srr_renderer_create_multi(const srr_scene* s, int n_devices, const int* device_ids, srr_renderer** out);
+/* Devices a renderer renders on (1 for srr_renderer_create), ids into
+ * device_ids[0 .. cap) (may be NULL). */
+int srr_renderer_devices(const srr_renderer* r, int* device_ids, int cap);
+/* The frame-end transport of a renderer: "rccl", "copy", or "none" (one device). */
+const char* srr_renderer_transport(const srr_renderer* r);
+/* The multi-device frame's bookkeeping, host only (no GPU): shard k's pixels are
+ * srr_shard_pixels({.., shard_index k, shard_count n_devices}); the gather packs
+ * the shards' slabs in shard order, so packed entry i is image pixel
+ * gather_index[i] (nx*ny entries, may be NULL) and shard k's slab starts at
+ * shard_offsets[k] (n_devices + 1 entries, may be NULL).  Returns nx*ny. */
+int64_t srr_multi_plan(const srr_params* p, int n_devices, int32_t* gather_index, int64_t* shard_offsets);
 /* Number of pixels this shard renders, and their PPM-order indices (row 0 =
  * top, Raytracing_n.cpp:873-876) into pixel_index[] (may be NULL). */
 int64_t srr_shard_pixels(const srr_params* p, int32_t* pixel_index);

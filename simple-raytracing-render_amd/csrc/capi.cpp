@@ -16,6 +16,7 @@
 #include "imageio.h"
 #include "meshio.h"
 #include "../../include/srr/merl.h"
+#include "multi.h"
 #include "renderer.h"
 
 using namespace srr;
@@ -345,6 +346,32 @@ int srr_renderer_create(const srr_scene* sc, int device, srr_renderer** out) {
 
 void srr_renderer_destroy(srr_renderer* r) { delete r; }
 
+int srr_renderer_create_multi(const srr_scene* sc, int n, const int* ids, srr_renderer** out) {
+  if (!sc || !out || !ids) return fail(SRR_EINVAL, "null argument");
+  std::string err;
+  int rc = multi_create(sc->s, n, ids, out, err);
+  if (rc < 0) return fail(rc, err);
+  return 0;
+}
+
+int srr_renderer_devices(const srr_renderer* r, int* ids, int cap) {
+  if (!r) return fail(SRR_EINVAL, "null renderer");
+  if (r->multi) return multi_devices(r->multi, ids, cap);
+  if (ids && cap > 0) ids[0] = r->device;
+  return 1;
+}
+
+const char* srr_renderer_transport(const srr_renderer* r) {
+  return !r ? "" : r->multi ? multi_transport(r->multi) : "none";
+}
+
+int64_t srr_multi_plan(const srr_params* p, int n, int32_t* index, int64_t* off) {
+  std::string err;
+  const int64_t rc = multi_plan(p, n, nullptr, index, off, err);
+  if (rc < 0) return fail((int)rc, err);
+  return rc;
+}
+
 int64_t srr_shard_pixels(const srr_params* p, int32_t* out) {
   if (!p || p->nx <= 0 || p->ny <= 0 || p->shard_count < 1 || p->shard_index < 0 ||
       p->shard_index >= p->shard_count)
@@ -378,6 +405,11 @@ int srr_render_device(srr_renderer* r, const srr_params* p, float* d_mean, srr_s
   if (p->spp < 1 || p->max_depth < 0 || p->max_depth > 64) return fail(SRR_EINVAL, "spp >= 1, 0 <= max_depth <= 64");
   if (p->sample_begin < 0 || p->sample_begin > INT32_MAX - p->spp)
     return fail(SRR_EINVAL, "sample_begin must be >= 0 and sample_begin + spp must fit in int32");
+  if (r->multi) {
+    std::string err;
+    const int rc = multi_render_device(r, p, d_mean, stats, err);
+    return rc < 0 ? fail(rc, err) : 0;
+  }
   // the shard's pixel list is built and uploaded once per shard (srr_renderer::pix_key)
   const int key[5] = {p->nx, p->ny, p->shard_index, p->shard_count, p->tile};
   const bool held = std::equal(key, key + 5, r->pix_key);
@@ -406,6 +438,11 @@ int srr_render_device_async(srr_renderer* r, const srr_params* p, float* d_mean,
   if (p->spp < 1 || p->max_depth < 0 || p->max_depth > 64) return fail(SRR_EINVAL, "spp >= 1, 0 <= max_depth <= 64");
   if (p->sample_begin < 0 || p->sample_begin > INT32_MAX - p->spp)
     return fail(SRR_EINVAL, "sample_begin must be >= 0 and sample_begin + spp must fit in int32");
+  if (r->multi) {
+    std::string err;
+    const int rc = multi_render_device_async(r, p, d_mean, ticket, err);
+    return rc < 0 ? fail(rc, err) : 0;
+  }
   const int key[5] = {p->nx, p->ny, p->shard_index, p->shard_count, p->tile};
   const bool held = std::equal(key, key + 5, r->pix_key);
   int64_t npix = held ? r->pix_n : srr_shard_pixels(p, nullptr);
@@ -431,14 +468,17 @@ int srr_render_device_async(srr_renderer* r, const srr_params* p, float* d_mean,
 int srr_render_wait(srr_renderer* r, int64_t ticket, srr_stats* stats) {
   if (!r) return fail(SRR_EINVAL, "null renderer");
   std::string err;
-  int rc = render_wait(r, ticket, stats, err);
+  int rc = r->multi ? multi_render_wait(r, ticket, stats, err) : render_wait(r, ticket, stats, err);
   if (rc < 0) return fail(rc, err);
   return 0;
 }
 
 int srr_render(srr_renderer* r, const srr_params* p, float* mean, unsigned char* rgb8, srr_stats* stats) {
   if (!r || !p) return fail(SRR_EINVAL, "null argument");
-  int64_t npix = srr_shard_pixels(p, nullptr);
+  if (r->multi && p->shard_count > 1)
+    return fail(SRR_EINVAL, "a multi-device renderer shards the frame itself: shard_count must be 0 or 1");
+  int64_t npix = r->multi ? (p->nx > 0 && p->ny > 0 ? (int64_t)p->nx * p->ny : -1) : srr_shard_pixels(p, nullptr);
+  if (npix < 0 && r->multi) return fail(SRR_EINVAL, "bad params");
   if (npix < 0) return (int)npix;
   float* d = nullptr;
   HIPCHK(hipSetDevice(r->device));
@@ -458,6 +498,7 @@ int srr_render(srr_renderer* r, const srr_params* p, float* mean, unsigned char*
 
 int srr_accum_get(srr_renderer* r, float* sums, int64_t* npix, int64_t* samples) {
   if (!r) return fail(SRR_EINVAL, "null renderer");
+  if (r && r->multi) return fail(SRR_EINVAL, "progressive sums and kept paths are per device: use a one-device renderer");
   if (npix) *npix = r->acc_npix;
   if (samples) *samples = r->acc_samples;
   if (sums && r->acc_npix) {
@@ -469,6 +510,7 @@ int srr_accum_get(srr_renderer* r, float* sums, int64_t* npix, int64_t* samples)
 
 int srr_accum_set(srr_renderer* r, const float* sums, int64_t npix, int64_t samples) {
   if (!r || !sums || npix <= 0 || samples < 0) return fail(SRR_EINVAL, "bad accumulator state");
+  if (r && r->multi) return fail(SRR_EINVAL, "progressive sums and kept paths are per device: use a one-device renderer");
   HIPCHK(hipSetDevice(r->device));
   drain_async(r);  // frames in flight read the pixel list this may reallocate
   if ((size_t)npix > r->pix_cap) {
@@ -490,6 +532,7 @@ int srr_accum_set(srr_renderer* r, const float* sums, int64_t npix, int64_t samp
 }
 
 int srr_copy_paths(srr_renderer* r, float* radiance, unsigned char* rays) {
+  if (r && r->multi) return fail(SRR_EINVAL, "progressive sums and kept paths are per device: use a one-device renderer");
   if (!r || !r->raw_all) return fail(SRR_EINVAL, "render with SRR_FLAG_KEEP_PATHS first");
   HIPCHK(hipSetDevice(r->device));
   if (radiance) HIPCHK(hipMemcpy(radiance, r->raw_all, r->kept_paths * 3 * sizeof(float), hipMemcpyDeviceToHost));

@@ -169,5 +169,7 @@ void launch_shade(const SceneView& S, const PathState& P, const int* lists, int 
                   hipStream_t st);
 void launch_accumulate(const PathState& P, const BatchInfo& B, float* acc, hipStream_t st);
 void launch_finish(const float* acc, float* mean, int64_t n, int ns, hipStream_t st);
+// image[index[i]] = packed[i] (float3 per pixel) for i < n: multi-device frame assembly
+void launch_scatter_pixels(const float* packed, const int32_t* index, int64_t n, float* image, hipStream_t st);
 
 }  // namespace srr

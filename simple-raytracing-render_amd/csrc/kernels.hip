@@ -3192,6 +3192,17 @@ __global__ void k_finish(const float* acc, float* mean, int64_t n, int ns) {
   mean[i] = acc[i] * k;
 }
 
+// Multi-device frame assembly (multi.cpp): the gathered shard slabs, packed in
+// shard order, scattered to their image pixels: image[index[i]] = packed[i]
+// (float3).  One thread per channel word, so the packed reads coalesce.
+__global__ void k_scatter_pixels(const float* __restrict__ packed, const int32_t* __restrict__ index, int64_t n,
+                                 float* __restrict__ image) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 3 * n) return;
+  const int64_t px = i / 3;
+  image[3 * (int64_t)index[px] + (i - 3 * px)] = packed[i];
+}
+
 // ------------------------------------------------------------ MERL lookup
 // brdf::lookup_brdf_val (brdf.h:190-214) for n direction pairs: one query per
 // thread, angles[4q..4q+3] = (theta_in, fi_in, theta_out, fi_out).
@@ -3514,6 +3525,12 @@ void launch_accumulate(const PathState& P, const BatchInfo& B, float* acc, hipSt
 void launch_finish(const float* acc, float* mean, int64_t n, int ns, hipStream_t st) {
   int64_t g = (3 * n + 255) / 256;
   hipLaunchKernelGGL(dev::k_finish, dim3((unsigned)g), dim3(256), 0, st, acc, mean, n, ns);
+}
+
+void launch_scatter_pixels(const float* packed, const int32_t* index, int64_t n, float* image, hipStream_t st) {
+  if (n <= 0) return;
+  const int64_t g = (3 * n + 255) / 256;
+  hipLaunchKernelGGL(dev::k_scatter_pixels, dim3((unsigned)g), dim3(256), 0, st, packed, index, n, image);
 }
 
 

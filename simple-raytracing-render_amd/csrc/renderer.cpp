@@ -1,6 +1,8 @@
 // Renderer: scene upload and the multi-lane wavefront driver (renderer.h).
 #include "renderer.h"
 
+#include "multi.h"
+
 #include <algorithm>
 #include <chrono>
 #include <cstdlib>
@@ -36,6 +38,10 @@ int renderer_create(const Scene& sc, int device, srr_renderer** out, std::string
   Flat F;
   int rc = flatten(sc, F, err);
   if (rc < 0) return rc;
+  return renderer_create_flat(F, device, out, err);
+}
+
+int renderer_create_flat(const Flat& F, int device, srr_renderer** out, std::string& err) {
   std::unique_ptr<srr_renderer> r(new srr_renderer());
   r->device = device;
   if (const char* e = getenv("SRR_LANES")) r->n_lanes = std::max(1, std::min(kMaxLanes, atoi(e)));
@@ -969,6 +975,10 @@ int render_device(srr_renderer* r, const srr_params* p, const int32_t* pix, int6
 }  // namespace srr
 
 srr_renderer::~srr_renderer() {
+  if (multi) {
+    srr::multi_destroy(multi);
+    multi = nullptr;
+  }
   (void)hipSetDevice(device);
   (void)hipDeviceSynchronize();
   for (void* p : scene_bufs) (void)hipFree(p);

@@ -80,10 +80,14 @@ struct DoneTicket {  // an async frame finished before its srr_render_wait
   std::string err;
 };
 
+struct Multi;  // multi.h
 }  // namespace srr
 
 struct srr_renderer {
   int device = 0;
+  // srr_renderer_create_multi: this handle renders over several devices through
+  // their own renderers (multi.cpp); its single-device state below stays unused
+  srr::Multi* multi = nullptr;
   srr::SceneView view{};
   std::vector<void*> scene_bufs;
   int n_lanes = 2;
@@ -129,6 +133,8 @@ struct srr_renderer {
 
 namespace srr {
 int renderer_create(const Scene& s, int device, srr_renderer** out, std::string& err);
+// the same from an already flattened scene (a multi-device renderer flattens once)
+int renderer_create_flat(const Flat& F, int device, srr_renderer** out, std::string& err);
 // pix: the shard's npix pixel indices, or nullptr when the renderer already holds
 // them (srr_renderer::pix_key)
 int render_device(srr_renderer* r, const srr_params* p, const int32_t* pix, int64_t npix, float* d_mean,

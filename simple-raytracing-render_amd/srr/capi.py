@@ -56,6 +56,12 @@ def lib():
         L.srr_scene_destroy.argtypes = [vp]
         L.srr_renderer_create.argtypes = [vp, ip, ctypes.POINTER(vp)]
         L.srr_renderer_destroy.argtypes = [vp]
+        L.srr_renderer_create_multi.argtypes = [vp, ip, vp, ctypes.POINTER(vp)]
+        L.srr_renderer_devices.argtypes = [vp, vp, ip]
+        L.srr_renderer_transport.argtypes = [vp]
+        L.srr_renderer_transport.restype = cp
+        L.srr_multi_plan.restype = ctypes.c_int64
+        L.srr_multi_plan.argtypes = [ctypes.POINTER(Params), ip, vp, vp]
         L.srr_shard_pixels.restype = ctypes.c_int64
         L.srr_shard_pixels.argtypes = [ctypes.POINTER(Params), vp]
         L.srr_render_device.argtypes = [vp, ctypes.POINTER(Params), vp, ctypes.POINTER(Stats)]
@@ -104,6 +110,16 @@ def shard_pixels(p: Params) -> np.ndarray:
     out = np.zeros(n, np.int32)
     lib().srr_shard_pixels(ctypes.byref(p), _ptr(out))
     return out
+
+
+def multi_plan(p: Params, n_devices: int) -> tuple[np.ndarray, np.ndarray]:
+    """srr_multi_plan (host only): the packed-frame order of an n-device frame --
+    (gather_index[nx*ny]: image pixel of each packed entry, shard_offsets[n+1])."""
+    total = _check(lib().srr_multi_plan(ctypes.byref(p), n_devices, None, None))
+    index = np.zeros(total, np.int32)
+    off = np.zeros(n_devices + 1, np.int64)
+    _check(lib().srr_multi_plan(ctypes.byref(p), n_devices, _ptr(index), _ptr(off)))
+    return index, off
 
 
 def sobol_points(n: int) -> np.ndarray:
@@ -165,15 +181,32 @@ class Merl:
 
 
 class Renderer:
-    """Flattened scene resident on HIP device `device` (srr_renderer_create)."""
+    """Flattened scene resident on HIP device `device` (srr_renderer_create), or
+    on every device of `devices` (srr_renderer_create_multi: the whole frame
+    rendered over all of them, gathered to devices[0] over RCCL)."""
 
-    def __init__(self, scene, device: int = 0):
+    def __init__(self, scene, device: int = 0, devices=None):
         if isinstance(scene, str):
             scene = Scene(scene)
         self.scene = scene
         h = ctypes.c_void_p()
-        _check(lib().srr_renderer_create(scene.h, device, ctypes.byref(h)))
+        if devices is None:
+            _check(lib().srr_renderer_create(scene.h, device, ctypes.byref(h)))
+        else:
+            ids = np.ascontiguousarray(devices, np.int32)
+            _check(lib().srr_renderer_create_multi(scene.h, ids.size, _ptr(ids), ctypes.byref(h)))
         self.h = h
+
+    def devices(self) -> list:
+        n = _check(lib().srr_renderer_devices(self.h, None, 0))
+        ids = np.zeros(n, np.int32)
+        lib().srr_renderer_devices(self.h, _ptr(ids), n)
+        return ids.tolist()
+
+    @property
+    def transport(self) -> str:
+        """"rccl" / "copy" (multi-device frame-end gather) or "none" (one device)."""
+        return lib().srr_renderer_transport(self.h).decode()
 
     def __del__(self):
         if getattr(self, "h", None):
@@ -185,7 +218,7 @@ class Renderer:
         paths[n,spp,3], rays[n,spp] when keep_paths)."""
         flags = kw.pop("flags", 0) | (FLAG_KEEP_PATHS if keep_paths else 0)
         p = make_params(nx, ny, spp, max_depth, flags=flags, **kw)
-        n = shard_pixels(p).size
+        n = nx * ny if self.transport != "none" else shard_pixels(p).size
         mean = np.zeros((n, 3), np.float32)
         img8 = np.zeros((n, 3), np.uint8)
         st = Stats()

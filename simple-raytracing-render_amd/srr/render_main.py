@@ -6,6 +6,7 @@ GPU, print the elapsed milliseconds and write the P3 PPM (the tone map and byte
 format of Raytracing_n.cpp:850-886).
 
     python -m srr.render_main [--sceneid 2] [--nx 1000] [--ny 1000] [--ns 50] [--max-depth 50] [--out out.ppm]
+                              [--gpus N]   (srr_renderer_create_multi: one RCCL gather at frame end)
 
 Defaults are the reference's globals (Raytracing_n.cpp:39-43).  Differences, all
 forced by the reference: its 8 render threads race on shared state
@@ -33,6 +34,8 @@ def parse(argv=None):
     ap.add_argument("--ns", type=int, default=50, help="samples per pixel")
     ap.add_argument("--max-depth", type=int, default=50)
     ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="render on devices device .. device+gpus-1 (pixels dealt round-robin, one RCCL gather)")
     ap.add_argument("--contents", default=None, help="the reference's contents/ directory (assets)")
     ap.add_argument("--out", default="out.ppm")
     return ap.parse_args(argv)
@@ -41,9 +44,10 @@ def parse(argv=None):
 def main(argv=None) -> int:
     a = parse(argv)
     sc = ref_scenes.BY_SCENEID[a.sceneid](float(a.nx) / float(a.ny), contents=a.contents)  # :894-919
-    r = capi.Renderer(sc.text(), device=a.device)
+    r = (capi.Renderer(sc.text(), device=a.device) if a.gpus == 1 else
+         capi.Renderer(sc.text(), devices=list(range(a.device, a.device + a.gpus))))
     t0 = time.perf_counter()
-    out = r.render(a.nx, a.ny, a.ns, a.max_depth)
+    out = r.render(a.nx, a.ny, a.ns, a.max_depth, tile=1)
     ms = (time.perf_counter() - t0) * 1e3
     print(f"{int(ms)}ms")  # :944-947
     capi.write_ppm(a.out, a.nx, a.ny, out["img8"])

@@ -95,3 +95,27 @@ def test_bench_rccl_leg_on_one_gpu(plan, tmp_path):
     assert "RCCL" in j2["config"]["workload"]
     assert j2["config"]["world_rays_per_step"] == j1["config"]["world_rays_per_step"]
     np.testing.assert_array_equal(np.load(f2).view(np.uint32), np.load(f1).view(np.uint32))
+
+
+@pytest.mark.parametrize("gpus", [1, 3])
+def test_bench_capi_host_leg(gpus, tmp_path):
+    """bench.py --host capi: ONE process renders the frame
+    over --gpus devices through srr_renderer_create_multi -- at 1 GPU with a real
+    RCCL communicator (ncclSend / ncclRecv to device 0), at 3 rehearsed on the one
+    leased GPU (the gather then copies).  Frame bitwise the plain one, world rays
+    equal, the line names the host, transport and devices."""
+    f1, f2 = str(tmp_path / "f1.npy"), str(tmp_path / "f2.npy")
+    one = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", *ARGS, "--save-frame", f1],
+                         capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert one.returncode == 0, one.stderr[-3000:]
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--host", "capi", "--gpus", str(gpus), *ARGS,
+           "--save-frame", f2] + (["--rehearse"] if gpus > 1 else [])
+    rc = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert rc.returncode == 0, rc.stderr[-3000:]
+    j1, j2 = _json_line(one.stdout), _json_line(rc.stdout)
+    print(f"capi host, {gpus} device(s):", j2["value"], j2["config"]["transport"], j2["config"]["workload"])
+    assert j2["n_gpus"] == gpus and j2["config"]["host"] == "capi"
+    assert j2["config"]["transport"] == ("rccl" if gpus == 1 else "copy")
+    assert j2["config"]["devices"] == [0] * gpus
+    assert j2["config"]["world_rays_per_step"] == j1["config"]["world_rays_per_step"]
+    np.testing.assert_array_equal(np.load(f2).view(np.uint32), np.load(f1).view(np.uint32))

@@ -52,7 +52,8 @@ def _rank_main(rank, world, port, plan, text, outdir, staged=False):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("plan,world,staged", [("tiles", 2, False), ("tiles", 3, False), ("samples", 2, False),
+@pytest.mark.parametrize("plan,world,staged", [("tiles", 2, False), ("tiles", 3, False), ("tiles", 8, False),
+                                               ("samples", 2, False), ("samples", 8, True),
                                                ("tiles", 2, True), ("samples", 2, True)])
 def test_multi_rank_frame_matches_single_render(plan, world, staged, tmp_path):
     """tiles: the gathered frame is bitwise the one-renderer frame; samples: the

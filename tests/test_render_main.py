@@ -108,3 +108,20 @@ def test_render_main_image_is_the_python_render(exe, tmp_path):
     ref = str(tmp_path / "want.ppm")
     capi.write_ppm(ref, nx, ny, want["img8"])
     assert open(out, "rb").read() == open(ref, "rb").read()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devs", ["0", "0,0,0"])
+def test_render_main_multi_device_image_is_the_one_device_image(exe, tmp_path, devs):
+    """render_main --devices (C++ host, srr_renderer_create_multi): "0" gathers
+    through a real RCCL communicator of one GPU, "0,0,0" deals three shards on the
+    leased GPU (device copies); the PPM is byte-identical to the one-device run."""
+    nx, ny, ns = 48, 40, 4
+    args = ["--scene", "s2", "--nx", str(nx), "--ny", str(ny), "--ns", str(ns)]
+    one, multi = str(tmp_path / "one.ppm"), str(tmp_path / "multi.ppm")
+    r = subprocess.run([exe, *args, "--out", one], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run([exe, *args, "--devices", devs, "--out", multi], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert ("(rccl)" if devs == "0" else "(copy)") in r.stderr, r.stderr
+    assert open(multi, "rb").read() == open(one, "rb").read()
