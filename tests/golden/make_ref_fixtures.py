@@ -7,13 +7,18 @@ distinct image.  reft_soldier_scene reuses soldier_scene.npz: the two scenes
 differ only in the camera's aspect, so only its camera line is stored.
 
 The large-mesh goldens (reft_cornell_box, reft_teapot_scene,
-reft_jadebunny_scene: 16-32 MB of triangles each) and refb_random_scene (six
-2048x2048 textures) stay CPU-only.
+reft_jadebunny_scene: 16-32 MB of triangles each as text) and refb_random_scene
+(six 2048x2048 textures) are not flattened: tests/golden/ref_assets.npz holds the
+asset FILES their builders read (bunny.ply LZMA-compressed, sky_2.png, the six
+sky_1 JPEGs: the reference's own data files, byte for byte), and
+tests/ref_fixtures.py lays them out as a contents/ directory for srr's builders
+(srr/ref_scenes.py) on hosts without /root/reference.
 
     python tests/golden/make_ref_fixtures.py      (development container)
 """
 import hashlib
 import json
+import lzma
 import os
 import re
 import sys
@@ -30,6 +35,14 @@ from make_soldier import pack  # noqa: E402
 from srr import ref_scenes  # noqa: E402
 
 OUT = os.path.join(HERE, "ref_scene_fixtures.npz")
+ASSETS_OUT = os.path.join(HERE, "ref_assets.npz")
+# the files the builders of the remaining goldens read (contents/-relative)
+ASSETS = ["models/bunny.ply", "environment_map/sky_2.png"] + [
+    f"environment_map/sky_1/{f}.jpg" for f in ("Front", "Back", "Left", "Right", "Top", "Bottom")]
+
+
+def asset_key(rel: str) -> str:
+    return "file_" + rel.replace("/", "__").replace(".", "_dot_")
 CONTENTS = "/root/reference/contents"
 KEYS = ["refb_ball_scenes", "refb_final", "reft_ball_orennayar_scenes", "reft_flatnormal_bunny"]
 
@@ -63,6 +76,14 @@ def main():
         arrays[k + "_shape"] = np.array(v.shape, np.int64)
     np.savez(OUT, **arrays)
     print(OUT, os.path.getsize(OUT), "bytes;", len(images), "images")
+    assets = {}
+    for rel in ASSETS:
+        data = open(os.path.join(CONTENTS, rel), "rb").read()
+        if rel.endswith(".ply"):
+            data = lzma.compress(data, preset=9 | lzma.PRESET_EXTREME)
+        assets[asset_key(rel)] = np.frombuffer(data, np.uint8)
+    np.savez(ASSETS_OUT, **assets)
+    print(ASSETS_OUT, os.path.getsize(ASSETS_OUT), "bytes;", len(assets), "asset files")
 
 
 if __name__ == "__main__":

@@ -51,3 +51,33 @@ def test_restatement_reproduces_c2_full_frame_rows():
     got["mean"] = out["img"]
     res = fullframe.compare(got, {k: v[pix] for k, v in want.items()})
     assert res["hash_mismatch_pixels"] == 0 and res["mean_mismatch_pixels"] == 0, res
+
+
+def test_fold_detects_one_changed_path_in_a_group():
+    m = fullframe.meta("s2_digest")
+    n = m["nx"] * m["ny"]
+    paths = np.fromfile(f"{ob.GOLDEN}/s2.paths.f32", np.float32).reshape(n, m["spp"], 3).copy()
+    rays = np.fromfile(f"{ob.GOLDEN}/s2.rays.u8", np.uint8).reshape(n, m["spp"]).copy()
+    want = fullframe.fold(fullframe.digest(paths, rays), 16)
+    paths[77, 5, 1] = np.nextafter(paths[77, 5, 1], np.float32(np.inf))
+    res = fullframe.compare(fullframe.digest(paths, rays), want)
+    assert res["hash_mismatch_groups"] == 1 and res["ray_mismatch_groups"] == 0 and res["first_bad_group"] == [4]
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("name", ["c4_full", "c5_full", "c4r_full"])
+def test_restatement_reproduces_1080p_full_frame_groups(name):
+    """The CPU restatement on 48 pixel groups (768 pixels x 16 samples) of each
+    1920x1080 reference frame (C4 / C5 stand-ins, C4_real) against the
+    reference's grouped digests."""
+    m = fullframe.meta(name)
+    want = fullframe.load(name)
+    g = want["group"]
+    groups = np.linspace(0, want["grays"].size - 1, 48).astype(np.int64)
+    pix = (groups[:, None] * g + np.arange(g)[None, :]).ravel().astype(np.int32)
+    out = ob.render(fullframe.scene_text(name), m["nx"], m["ny"], m["spp"], m["max_depth"], pixels=pix, threads=8)
+    got = fullframe.fold(fullframe.digest(out["paths"], out["rays"]), g)
+    assert np.array_equal(got["grays"], want["grays"][groups])
+    assert np.array_equal(got["ghash"], want["ghash"][groups])

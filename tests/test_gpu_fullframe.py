@@ -65,3 +65,26 @@ def test_c2_full_frame_is_the_reference_frame(mode, monkeypatch):
     pc = parity.compare_paths(out["paths"][tp], gp)
     assert pc["bitexact"] == 1.0, pc
     assert (out["rays"][tp] == gr).all()
+
+
+@pytest.mark.parametrize("name", ["c4_full", "c5_full", "c4r_full"])
+def test_1080p_full_frame_is_the_reference_frame(name):
+    """The 1920x1080 configs' WHOLE frames at 16 spp (33 M paths each): C4 and
+    C5 (the BASELINE stand-ins with the 102,400-triangle mesh; C5 adds the fog)
+    and C4_real (the reference's own soldier_scene, Raytracing_n.cpp:585-657,
+    from its committed fixture), every path's radiance bits and world rays
+    against the reference's own render (grouped digests, tests/fullframe.fold)."""
+    m = fullframe.meta(name)
+    want = fullframe.load(name)
+    r = capi.Renderer(fullframe.scene_text(name))
+    out = r.render(m["nx"], m["ny"], m["spp"], m["max_depth"], keep_paths=True)
+    got = fullframe.digest(out["paths"], out["rays"])
+    res = fullframe.compare(got, want)
+    res["stats_world_rays"] = out["stats"]["world_rays"]
+    print(name, res)
+    if res["hash_mismatch_groups"] or res["ray_mismatch_groups"]:
+        g = want["group"]
+        bad_groups = np.flatnonzero(fullframe.fold(got, g)["ghash"] != want["ghash"])
+        _save_diag(name, (bad_groups[:, None] * g + np.arange(g)[None, :]).ravel(), out)
+    assert out["stats"]["world_rays"] == m["world_rays"], res
+    assert res["ray_mismatch_groups"] == 0 and res["hash_mismatch_groups"] == 0, res

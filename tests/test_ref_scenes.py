@@ -7,9 +7,11 @@ restated in srr/ref_scenes.py.
   the goldens the REFERENCE made (tests/golden/make_scenes.py): refb_* from the
   reference's builder functions themselves, reft_* from the reference's classes
   built from the same scene text.
-* GPU (no reference files on the box): every builder with stand-in assets of
-  the same names and sizes (generated images, small generated meshes), the HIP
-  path through the C-ABI against the CPU restatement.
+* GPU (no reference files on the box): all nine goldens from the committed
+  fixtures (tests/ref_fixtures.py: flattened scenes, or the builders run on the
+  reference's asset files from tests/golden/ref_assets.npz), the HIP path bit
+  for bit against the reference's paths; and every builder with stand-in assets
+  of the same names and sizes against the CPU restatement.
 """
 import json
 import os
