@@ -11,6 +11,7 @@ import os
 
 import numpy as np
 import pytest
+import torch  # noqa: F401  (before libsrr's first HIP call: torch then brings its own HIP runtime)
 
 from srr import capi, scenes
 
