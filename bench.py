@@ -37,9 +37,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--scene", default="s2", choices=["s1", "s2", "s3", "s3_metal", "s4", "s5", "s4_real"],
+    ap.add_argument("--scene", default="s2",
+                    choices=["s1", "s2", "s3", "s3_metal", "s4", "s5", "s4_real", "ball", "random"],
                     help="s4_real: the reference's real soldier_scene (Soilder.FBX, sky4.jpg; Raytracing_n.cpp:585-657) "
-                         "from its committed fixture (tests/golden/make_soldier.py), 1920x1080x1024")
+                         "from its committed fixture (tests/golden/make_soldier.py), 1920x1080x1024; ball: the "
+                         "reference's as-shipped default run, sceneid 2 ball_scenes at its globals 1000x1000x50 "
+                         "(Raytracing_n.cpp:39-43, :379-425); random: random_scene (~490 spheres, the global-memory "
+                         "world variant of k_paths) at the same globals")
     ap.add_argument("--divs", type=int, default=0,
                     help="teapot subdivision (s2/s3: 10 = 6,400 tris; 100 = the reference's as-shipped 640,000, "
                          "teapot.h:77; s4/s5: 40 = 102,400)")
@@ -81,7 +85,8 @@ def parse():
     return ap.parse_args()
 
 
-CONFIG_KEY = {"s1": "C1", "s2": "C2", "s3": "C3", "s3_metal": "C3_metal", "s4": "C4", "s5": "C5", "s4_real": "C4_real"}
+CONFIG_KEY = {"s1": "C1", "s2": "C2", "s3": "C3", "s3_metal": "C3_metal", "s4": "C4", "s5": "C5", "s4_real": "C4_real",
+              "ball": "REF_ball_scenes", "random": "REF_random_scene"}
 
 
 class _TextScene:
@@ -97,13 +102,42 @@ def _soldier_real():
     return _TextScene(soldier_fixture.scene_text()), dict(nx=1920, ny=1080, spp=1024, max_depth=50)
 
 
+def _ref_builder(name):
+    """One of the reference's own scene builders (srr/ref_scenes.py, pinned to the
+    reference's builder code) at the reference's globals nx = ny = 1000, ns = 50,
+    maxDepth 50 (Raytracing_n.cpp:39-43), on its asset files (/root/reference/contents
+    here, tests/golden/ref_assets.npz on the GPU box)."""
+    from srr import ref_scenes
+    contents = "/root/reference/contents"
+    if not os.path.isdir(contents):
+        import ref_fixtures
+        contents = ref_fixtures.contents_dir()
+    return ref_scenes.BUILDERS[name](1000 / 1000, contents), dict(nx=1000, ny=1000, spp=50, max_depth=50)
+
+
+def host_cpus():
+    """The host CPUs this process may run on: nproc (sched_getaffinity), capped by
+    the cgroup CPU quota (cpu.max) when one is set -- on the GPU box the whole
+    machine's CPUs are visible (os.cpu_count()) but a job's share is its quota."""
+    nproc = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    return {"use": min(nproc, quota) if quota else nproc, "nproc": nproc, "cpu_count": os.cpu_count(),
+            "cgroup_quota_cpus": quota}
+
+
 def cpu_baseline(text, nx, ny, spp, budget_s):
     """The CPU restatement (oracle/liboracle.so, bit-identical to the
     reference) on a bounded pixel sample of the same frame."""
     import numpy as np
 
     import oracle_bind as ob
-    threads = min(16, os.cpu_count() or 1)
+    threads = host_cpus()["use"]
     rng = np.random.default_rng(1)
     # calibrate on a small sample, then size the timed sample to ~budget_s
     n_cal = min(nx * ny, 4096)
@@ -135,7 +169,8 @@ def cpu_baseline_reference(text, nx, ny, spp, max_depth, budget_s):
     harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
     if not os.access(harness, os.X_OK):
         return None
-    procs = min(16, os.cpu_count() or 1)
+    cpus = host_cpus()
+    procs = cpus["use"]
     npix = nx * ny
     with tempfile.TemporaryDirectory() as td:
         scene = os.path.join(td, "scene.txt")
@@ -161,10 +196,10 @@ def cpu_baseline_reference(text, nx, ny, spp, max_depth, budget_s):
     rays = sum(o["world_rays"] for o in outs)
     pixels = sum(o["pixels"] for o in outs)
     what = "the whole frame" if step == 1 else f"every {step}th pixel ({pixels} pixels)"
-    return {"value": rays / dt / 1e6, "unit": "Msamples/s", "cores": procs, "kind": "reference",
+    return {"value": rays / dt / 1e6, "unit": "Msamples/s", "cores": procs, "kind": "reference", "host_cpus": cpus,
             "sample": f"{what} of the {nx}x{ny} frame x {spp} spp ({rays} world rays, {dt:.1f} s): the "
                       f"reference's own color() (oracle/_ref/ref_harness, built from Raytracing_n.cpp), "
-                      f"one single-threaded process per core"}
+                      f"one single-threaded process per host CPU available to the job"}
 
 
 def bench_line(a, text, cfg, nx, ny, spp, rays_total, elapsed, trace_ms, launches, world, workload_tail,
@@ -217,6 +252,8 @@ def bench_line(a, text, cfg, nx, ny, spp, rays_total, elapsed, trace_ms, launche
         "dtype": "f32",
         "data": ("the reference's own assets (Soilder.FBX mesh 0, sky4.jpg, textures) via the committed fixture"
                  if a.scene == "s4_real" else
+                 "the reference's own scene builder and asset files (sky_2.png / sky_1 JPEGs)"
+                 if a.scene in ("ball", "random") else
                  "synthetic (scene built in code: Cornell box + tessellated Utah teapot)"),
         "config": dict({"workload": f"{key}: {a.scene}{f' divs {a.divs}' if a.divs else ''} {nx}x{ny} {spp}spp "
                                     f"maxDepth {cfg['max_depth']}" + workload_tail,
@@ -388,13 +425,14 @@ def main():
     host_reduce = use_dist and backend == "gloo"
 
     dv = {"divs": a.divs} if a.divs else {}
-    if a.divs and a.scene in ("s1", "s4_real"):
+    if a.divs and a.scene in ("s1", "s4_real", "ball", "random"):
         raise SystemExit(f"--divs: {a.scene} has no teapot")
     fac = {"s1": scenes.s1_cornell, "s2": lambda: scenes.s2_cornell_teapot(**dv),
            "s3": lambda: scenes.s3_cornell_teapot_microfacet(**dv),
            "s3_metal": lambda: scenes.s3_cornell_teapot_microfacet("metal", **dv),
            "s4": lambda: scenes.s4_soldier_standin(**dv), "s5": lambda: scenes.s5_soldier_fog(**dv),
-           "s4_real": _soldier_real}[a.scene]
+           "s4_real": _soldier_real, "ball": lambda: _ref_builder("ball_scenes"),
+           "random": lambda: _ref_builder("random_scene")}[a.scene]
     sc, cfg = fac()
     nx, ny, spp = a.nx or cfg["nx"], a.ny or cfg["ny"], a.spp or cfg["spp"]
     text = sc.text()

@@ -7,7 +7,7 @@ excluded) and the algorithmic bytes per sample they imply:
 Counted by the CPU restatement (oracle/restate.cpp), which test_oracle_pins.py
 pins bit-exact to the reference.  Writes tests/golden/traversal_counts.json.
 
-    python tests/golden/make_counts.py
+    python tests/golden/make_counts.py [config ...]     (default: all)
 """
 import json
 import os
@@ -20,7 +20,9 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 import oracle_bind as ob  # noqa: E402
 import soldier_fixture  # noqa: E402
-from srr import scenes  # noqa: E402
+from srr import ref_scenes, scenes  # noqa: E402
+
+CONTENTS = "/root/reference/contents"
 
 CONFIGS = {
     "C1": (scenes.s1_cornell, 96, 96, 16),
@@ -33,6 +35,10 @@ CONFIGS = {
     "C2_d100": (lambda: scenes.s2_cornell_teapot(divs=100), 96, 96, 16),
     # the reference's real soldier_scene (Raytracing_n.cpp:585-657) from its fixture
     "C4_real": (lambda: (_Text(soldier_fixture.scene_text()), None), 192, 108, 8),
+    # the reference's as-shipped default run (sceneid 2 ball_scenes, Raytracing_n.cpp:39-43, :379-425)
+    # and random_scene, through the reference's own builders (srr/ref_scenes.py) and assets
+    "REF_ball_scenes": (lambda: (ref_scenes.ball_scenes(1.0, CONTENTS), None), 96, 96, 16),
+    "REF_random_scene": (lambda: (ref_scenes.random_scene(1.0, CONTENTS), None), 96, 96, 16),
 }
 
 
@@ -45,8 +51,10 @@ class _Text:
 
 
 def main():
-    out = {}
-    for name, (fac, nx, ny, spp) in CONFIGS.items():
+    path = os.path.join(HERE, "traversal_counts.json")
+    out = json.load(open(path)) if os.path.exists(path) and sys.argv[1:] else {}
+    for name in sys.argv[1:] or CONFIGS:
+        fac, nx, ny, spp = CONFIGS[name]
         sc, _ = fac()
         r = ob.render(sc.text(), nx, ny, spp, 50, threads=os.cpu_count() or 4, want_paths=False)
         w, node, tri, prim = (int(x) for x in r["stats"][:4])
