@@ -233,9 +233,10 @@ int srr_render_device(srr_renderer* r, const srr_params* p, float* d_mean, srr_s
  * a third frame first finishes the oldest (its stats stay for its wait).
  * Device memory: each frame in flight holds its own sample window (all shard
  * pixels x the window's samples x 12 B, at most SRR_WINDOW_MB, default 8 GiB),
- * bounce records (16 B x max_depth per persistent lane) and sums; the async
- * slots and the synchronous slot never hold windows at the same time (switching
- * modes frees the other's). */
+ * bounce records (16 B x max_depth per persistent lane) and sums; the
+ * synchronous slot keeps its own window too, so alternating the two modes
+ * reallocates nothing (the other mode's windows are given back only when an
+ * allocation would run the device out of memory). */
 int srr_render_device_async(srr_renderer* r, const srr_params* p, float* d_mean, int64_t* ticket);
 /* Wait for an async frame and return its stats (each ticket once). */
 int srr_render_wait(srr_renderer* r, int64_t ticket, srr_stats* stats);

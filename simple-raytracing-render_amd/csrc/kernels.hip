@@ -2539,8 +2539,13 @@ constexpr int kRingWords = 11;  // o.xyz, d.xyz, time, lcg (2 words), pcg (2 wor
 // per lane) + the node cache <= 160 KB (344 nodes at kStack 8)
 constexpr int kPathsLdsNodesBig =
     (160 * 1024 - 8192 - 8 * kPathsLdsStack * 1024 - 1024 - (SRR_RAYRING ? 4 * kRingWords * 1024 : 0)) / 128;
-// 256-lane blocks (4 per CU, <= 40 KB each): the ring displaces the node cache,
-// which only meshes use and these blocks serve mesh-free scenes (renderer.cpp)
+// 256-lane blocks (4 per CU, <= 40 KB each) of the LDS-world variant: the ring
+// displaces the node cache.  These blocks serve mesh-free scenes by default
+// (paths_block_lanes); mesh scenes reach them only with SRR_BIGBLOCK=0 (an A/B
+// knob).  The two other 256-lane variants that serve mesh scenes keep the whole
+// cache: the global-world one (world tables beyond kWorldLdsBytes) has the 8 KB
+// of the LDS world to spare (16 KB stacks + 11 KB ring + 12 KB nodes), and the
+// quad-cooperative one (SRR_QUAD) runs without the ring.
 constexpr int kPathsLdsNodesSmall = SRR_RAYRING ? 8 : kPathsLdsNodes;
 
 // The camera ray of path index idx of the window (pixel-major: idx = lp * spp_w + s)
@@ -2639,8 +2644,8 @@ __global__ void __launch_bounds__(BS, MINB) k_paths(PathsArgs A) {
   const auto work = []() { return PathWork(paths_args()->W); };
   __shared__ int s_node[kStack * BS];
   __shared__ float s_t[kStack * BS];
-  constexpr bool RING = SRR_RAYRING;
-  constexpr int kNodesLds = BS == 1024 ? kPathsLdsNodesBig : kPathsLdsNodesSmall;
+  constexpr bool RING = SRR_RAYRING && !QUAD;
+  constexpr int kNodesLds = BS == 1024 ? kPathsLdsNodesBig : ((WL && RING) ? kPathsLdsNodesSmall : kPathsLdsNodes);
   __shared__ float4 s_n4[kNodesLds * 8];
   // RING: the wave's camera-ray ring, SoA [kRingWords][BS]; the wave's 64 entries
   // are its own lanes' columns (entry e of wave v at column 64 v + e)

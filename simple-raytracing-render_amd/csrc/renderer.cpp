@@ -348,6 +348,15 @@ void slot_free(FrameSlot& F) {
   F = FrameSlot{};
 }
 
+// frees a slot's sample window (the largest per-frame buffer); the next frame
+// on the slot allocates it again
+static void release_window(FrameSlot& F) {
+  if (!F.sample) return;
+  (void)hipFree(F.sample);
+  F.sample = nullptr;
+  F.sample_cap = 0;
+}
+
 // Path-resident engine (kernels.hip k_paths): one persistent kernel per window
 // of samples; samples land in a [pixel][sample] buffer that k_accumulate_window
 // sums per pixel in sample order, so the image is bitwise the wavefront engine's.
@@ -390,7 +399,21 @@ static int paths_enqueue(srr_renderer* r, FrameSlot& F, const srr_params* p, boo
     (void)hipFree(F.sample);
     F.sample = nullptr;
     F.sample_cap = 0;
-    RCHK(hipMalloc((void**)&F.sample, win_paths * 3 * sizeof(float)));
+    hipError_t e = hipMalloc((void**)&F.sample, win_paths * 3 * sizeof(float));
+    if (e == hipErrorOutOfMemory) {
+      // the synchronous slot and the two async slots each keep their window across
+      // mode switches (at most 3 x SRR_WINDOW_MB of the 288 GB); only when the device
+      // runs out are the other mode's windows given back
+      (void)hipGetLastError();
+      if (&F == &r->sync_slot) {
+        drain_async(r);
+        for (FrameSlot& A : r->async_slots) release_window(A);
+      } else {
+        release_window(r->sync_slot);
+      }
+      e = hipMalloc((void**)&F.sample, win_paths * 3 * sizeof(float));
+    }
+    RCHK(e);
     F.sample_cap = win_paths;
   }
   RCHK(hipMemsetAsync(F.ctr, 0, 16 * sizeof(unsigned long long), st));
@@ -565,15 +588,6 @@ static int paths_finish(srr_renderer* r, FrameSlot& F, const srr_params* p, srr_
   return 0;
 }
 
-// frees a slot's sample window (the largest per-frame buffer); the next frame
-// on the slot allocates it again
-static void release_window(FrameSlot& F) {
-  if (!F.sample) return;
-  (void)hipFree(F.sample);
-  F.sample = nullptr;
-  F.sample_cap = 0;
-}
-
 static void finish_slot(srr_renderer* r, FrameSlot& F) {
   F.busy = false;
   srr_params none{};
@@ -621,12 +635,6 @@ static int render_paths(srr_renderer* r, const srr_params* p, const int32_t* pix
     r->kept_paths = (int64_t)need;
   }
   FrameSlot& F = r->sync_slot;
-  // one sample window per mode: synchronous frames release the async slots' windows
-  // (each up to SRR_WINDOW_MB) instead of holding three
-  if (r->async_slots[0].sample || r->async_slots[1].sample) {
-    drain_async(r);
-    for (FrameSlot& A : r->async_slots) release_window(A);
-  }
   {
     const int rc = slot_init(F, r->acc_st, err);
     if (rc < 0) return rc;
@@ -672,7 +680,6 @@ int render_device_async(srr_renderer* r, const srr_params* p, const int32_t* pix
   RCHK(hipSetDevice(r->device));
   FrameSlot& F = r->async_slots[r->next_ticket % 2];
   if (F.busy) finish_slot(r, F);  // the slot's previous frame has not been waited for: finish it now
-  release_window(r->sync_slot);   // (idle: synchronous frames return finished)
   bool identity = false;
   {
     const int rc = paths_stage(r, p, pix, npix, identity, err);

@@ -83,3 +83,20 @@ def test_async_refuses_progressive_and_kept_paths():
         with pytest.raises(capi.SrrError):
             r.render_device_async(q, bufs[0].data_ptr())
     torch.cuda.synchronize()
+
+
+def test_alternating_sync_and_async_frames_keep_their_windows():
+    """Synchronous and pipelined frames interleaved frame by frame: each
+    mode keeps its sample window across the switches, every frame bitwise the
+    same."""
+    import torch
+    r, p, bufs = _setup(40, 24, 8)
+    r.render_device(p, bufs[0].data_ptr())
+    torch.cuda.synchronize()
+    want = _bits(bufs[0])
+    for k in range(3):
+        t = r.render_device_async(p, bufs[1].data_ptr())
+        r.render_device(p, bufs[2].data_ptr())
+        r.wait(t)
+        np.testing.assert_array_equal(_bits(bufs[1]), want)
+        np.testing.assert_array_equal(_bits(bufs[2]), want)
