@@ -117,7 +117,14 @@ int srr_scene_digest(const srr_scene* s, uint64_t* out, uint64_t* parts) {
   vec(f.tri_pos);
   vec(f.tri_shade);
   vec(f.media);
-  vec(f.obvhs);
+  {  // object BVHs, with the sphere groups and their items (device_scene.h DSGroup) in the same part
+    std::vector<uint8_t> b;
+    auto put = [&b](const void* p, size_t n) { b.insert(b.end(), (const uint8_t*)p, (const uint8_t*)p + n); };
+    put(f.obvhs.data(), f.obvhs.size() * sizeof(DObvh));
+    put(f.sgroups.data(), f.sgroups.size() * sizeof(DSGroup));
+    put(f.sg_items.data(), f.sg_items.size() * sizeof(DSGItem));
+    vec(b);
+  }
   vec(f.obvh_children);
   vec(f.mats);
   vec(f.texs);

@@ -36,6 +36,7 @@ enum ObjKind : int32_t {
   OBJ_MESH = 4,
   OBJ_MEDIUM = 5,
   OBJ_OBVH = 6,  // bvh_node over analytic hitables (spheres, boxes, rects, ...)
+  OBJ_SGROUP = 7,  // a run of consecutive plain spheres of a hitable_list behind a BVH (DSGroup)
 };
 
 enum XformKind : int32_t { XF_FLIP = 0, XF_TRANSLATE = 1, XF_ROTY = 2, XF_ROTX = 3 };
@@ -102,6 +103,33 @@ struct DObvh {
 
 struct DObvhChild {
   int32_t obj_begin, obj_count;  // into the DObj table
+};
+
+// A run of >= kSGroupMinRun consecutive spheres / moving spheres of a
+// hitable_list (random_scene's ~480, ball_scenes' 121), with no instance wrapper,
+// replaced in the list by one object: a BVH over their boxes (threaded preorder
+// records in the mesh BVH2 format of `nodes`, whose leaves name 1-2 items) gives
+// the same answer as testing them in order.  In hitable_list::hit
+// (hitable_list.h:21-33) sphere j reports its first root above t_min --
+// v_j = temp1 if temp1 > t_min, else temp2 if temp2 > t_min (sphere.h:36-66, temp1
+// <= temp2) -- and replaces the record iff v_j < closest_so_far: the run yields
+// the smallest v_j below the closest-so-far it was entered with, ties to the
+// EARLIEST sphere, whatever order the candidates are met in (kernels.hip
+// sgroup_hit).  Boxes and pruning are conservative (the float roots of a
+// near-tangent ray can lie ~1e-3 x distance off the sphere).
+constexpr int kSGroupMinRun = 8;
+
+struct DSGroup {
+  int32_t node_off, n_nodes;  // threaded BVH2 records in `nodes` (leaf code: (first item << 1) | (count - 1))
+  int32_t item_off, n_items;  // into sg_items, in BVH leaf order
+};
+
+struct DSGItem {   // one sphere of a run
+  DSphere s;
+  int32_t pos;     // its place in the run (ties go to the smaller)
+  int32_t moving;  // moving_sphere (center at the ray's time)
+  int32_t obj;     // its DObj (kept after the world list, for the hit record)
+  int32_t pad;
 };
 
 struct DMedium {  // constant_medium.h:4-50

@@ -33,6 +33,8 @@ struct SceneView {  // device pointers into the flattened tables (device_scene.h
   const DMedium* media;
   const DObvh* obvhs;                 // object BVHs (global memory)
   const DObvhChild* obvh_children;
+  const DSGroup* sgroups;             // sphere runs behind a BVH (global memory)
+  const DSGItem* sg_items;
   const DMat* mats;
   const DTex* texs;
   const uint8_t* images;

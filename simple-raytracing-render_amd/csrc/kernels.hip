@@ -257,7 +257,9 @@ struct TraceCtx {
   int slot = 0;
   // SRR_TIMING diagnostics (wave-uniform): cycles inside mesh traversals, steps
   mutable uint64_t mesh_cycles = 0;
-  mutable int mesh_steps = 0;
+  mutable int mesh_steps = 0;       // node steps of the wave's longest walk
+  mutable int mesh_lane_steps = 0;  // node steps summed over the wave's lanes
+  mutable int mesh_walkers = 0;     // lanes that took a node step
 #ifdef SRR_SLOW_RAYS
   mutable int last_steps = 0;  // diagnostics build: node steps | 1 << 30 on overflow, of this lane's last walk
 #endif
@@ -630,9 +632,15 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
     if ((int)__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) atomicAdd(cx.ctr + 67 + min(wmax, 63), 1ull);
   }
   if (TIMING) {
-    int st = (int)(nbox / 4);
-    for (int o = 32; o > 0; o >>= 1) st = max(st, __shfl_xor(st, o));
+    int st = (int)(nbox / 4), sum = st, walk = st > 0;
+    for (int o = 32; o > 0; o >>= 1) {
+      st = max(st, __shfl_xor(st, o));
+      sum += __shfl_xor(sum, o);
+      walk += __shfl_xor(walk, o);
+    }
     cx.mesh_steps += st;
+    cx.mesh_lane_steps += sum;
+    cx.mesh_walkers += walk;
     cx.mesh_cycles += __builtin_amdgcn_s_memtime() - tm_enter;
   }
   if (cx.ovf && cx.gst) {  // traversals that used the global stack (one atomic per wave)
@@ -1009,6 +1017,78 @@ SRR_D bool obvh_hit(const SceneView& S, const DObvh& o, const Ray& r, float tmin
   return found;
 }
 
+// A run of spheres behind a BVH (device_scene.h DSGroup): the result of testing
+// them in list order -- hitable_list.h:21-33 with sphere.h:36-66 -- found in any
+// order.  Sphere j's value is its first root above tmin, v_j = temp1 if temp1 >
+// tmin else temp2 if temp2 > tmin (computed exactly as sphere_hit does); the run
+// returns the smallest v_j < tmax, ties to the earliest sphere (a later equal
+// root fails sphere_hit's `temp < t_max`).  Boxes only prune, so they are padded
+// per ray by 4e-3 of the L1 distance from the ray origin to the box: a
+// near-tangent ray's float root can lie ~sqrt(10 eps) |oc| ~ 1.1e-3 |oc| off the
+// sphere (the cancellation in b*b - a*c), and a subtree is skipped only when its
+// padded entry lies beyond 1.0625 x the current bound.  NaN slab terms leave the
+// interval as it is (never reject).  Returns the winner's item index.
+template <int TR>
+SRR_D bool sgroup_hit(const SceneView& S, const DSGroup& g, const Ray& r, float tmin, float tmax, float& out_t,
+                      int& out_item) {
+  const V3 inv = v3(__frcp_rn(r.d.x), __frcp_rn(r.d.y), __frcp_rn(r.d.z));  // (pruning only)
+  bool found = false;
+  float best = tmax;
+  int best_pos = 0, best_item = -1;
+  const int end = g.node_off + g.n_nodes;
+  for (int node = g.node_off; node < end;) {
+    const float4 lo = S.nodes[2 * node], hi = S.nodes[2 * node + 1];
+    const int skip = __float_as_int(lo.w), leaf = __float_as_int(hi.w);
+    const float pad = 4e-3f * (fabsf(r.o.x - 0.5f * (lo.x + hi.x)) + fabsf(r.o.y - 0.5f * (lo.y + hi.y)) +
+                               fabsf(r.o.z - 0.5f * (lo.z + hi.z)) + (hi.x - lo.x) + (hi.y - lo.y) + (hi.z - lo.z));
+    float tn = -INFINITY, tf = INFINITY;
+#define SRR_AX(A)                                         \
+  {                                                       \
+    const float t0 = (lo.A - pad - r.o.A) * inv.A;        \
+    const float t1 = (hi.A + pad - r.o.A) * inv.A;        \
+    const bool sw = inv.A < 0.0f;                         \
+    const float n_ = sw ? t1 : t0, f_ = sw ? t0 : t1;     \
+    tn = n_ > tn ? n_ : tn;                               \
+    tf = f_ < tf ? f_ : tf;                               \
+  }
+    SRR_AX(x) SRR_AX(y) SRR_AX(z)
+#undef SRR_AX
+    const bool hit = !(tf < tn) && !(tn > best * kPruneSlack);
+    if (hit && leaf >= 0) {
+      const int first = leaf >> 1, count = (leaf & 1) + 1;
+      for (int i = first; i < first + count; ++i) {
+        const DSGItem it = S.sg_items[i];
+        const V3 oc = r.o - sphere_center(it.s, r.tm, it.moving != 0);  // sphere_hit's arithmetic
+        const float a = dot(r.d, r.d);
+        const float b = dot(oc, r.d);
+        const float c = dot(oc, oc) - it.s.r * it.s.r;
+        const float disc = b * b - a * c;
+        if (!(disc > 0)) continue;
+        const float sq = rsqrt_exact(disc);
+        const float t1 = (-b - sq) / a;
+        float v;
+        if (t1 > tmin) v = t1;
+        else {
+          const float t2 = (-b + sq) / a;
+          if (!(t2 > tmin)) continue;
+          v = t2;
+        }
+        if (!(v < tmax)) continue;
+        if (!found || v < best || (v == best && it.pos < best_pos)) {
+          found = true;
+          best = v;
+          best_pos = it.pos;
+          best_item = i;
+        }
+      }
+    }
+    node = (hit && leaf < 0) ? node + 1 : skip;
+  }
+  out_t = best;
+  out_item = best_item;
+  return found;
+}
+
 // hit of one non-medium flattened object (in its local frame)
 template <int TR, bool U = false>
 SRR_D bool basic_hit(const SceneView& S, const DObj& ob, const Ray& lr, float tmin, float tmax, bool is_medium,
@@ -1036,6 +1116,8 @@ SRR_D bool basic_hit(const SceneView& S, const DObj& ob, const Ray& lr, float tm
     }
     case OBJ_OBVH:
       return obvh_hit<TR>(S, S.obvhs[ob.idx], lr, tmin, tmax, is_medium, h.t, h.prim);
+    case OBJ_SGROUP:
+      return sgroup_hit<TR>(S, S.sgroups[ob.idx], lr, tmin, tmax, h.t, h.prim);
     case OBJ_MEDIUM:
       return false;
     default:
@@ -1274,8 +1356,8 @@ SRR_D HitRec world_record(const SceneView& S, const Ray& r, const WorldHit& w) {
   HitRec h;
   h.u = 0;  // moving_sphere / constant_medium leave u, v unset in the reference;
   h.v = 0;  // defined here as 0
-  if (ob.kind == OBJ_OBVH) {  // the primitive inside the object BVH, then the node's chain
-    const DObj& in = S.objs[w.prim];
+  if (ob.kind == OBJ_OBVH || ob.kind == OBJ_SGROUP) {  // the primitive inside, then the node's chain
+    const DObj& in = S.objs[ob.kind == OBJ_SGROUP ? S.sg_items[w.prim].obj : w.prim];
     prim_record<TR>(S, in, chain_in<TR>(S, in, lr), w.t, -1, h);
     chain_out(S, in, h.p, h.n);
   } else {
@@ -1303,6 +1385,7 @@ SRR_D int family_of(int mat, int kind, int depth, int max_depth) {
 SRR_D int hit_material(const SceneView& S, const WorldHit& w) {
   DObj ob = S.objs[w.obj];
   if (ob.kind == OBJ_OBVH) ob = S.objs[w.prim];
+  else if (ob.kind == OBJ_SGROUP) ob = S.objs[S.sg_items[w.prim].obj];
   switch (ob.kind) {
     case OBJ_SPHERE:
     case OBJ_MSPHERE: return S.spheres[ob.idx].mat;
@@ -2616,6 +2699,11 @@ __global__ void __launch_bounds__(BS, MINB) k_paths(PathsArgs A) {
   (void)A;  // read through paths_args()
   // TIMED (diagnostics): per-wave cycles in refill / world hit (mesh part) / record+scatter / fold
   uint64_t tp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // TIMED family diagnostics -> W.counters[16..27]: ticks in the BECK / SPEC / DIFF-set-up
+  // branches of the per-lane scatter, iterations each branch ran, lanes it ran for;
+  // lanes in a path; the longest walk's node steps, all lanes' steps, walking lanes (wave time
+  // in the mesh is tp[2])
+  uint64_t tf[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t it = 0;
   // WL: world tables staged in LDS (they fit in kWorldLdsBytes); otherwise read
   // from global memory (large object lists, e.g. random_scene's ~490 spheres)
@@ -2781,6 +2869,7 @@ __global__ void __launch_bounds__(BS, MINB) k_paths(PathsArgs A) {
       nxt_armed = true;
     }
     if (__ballot(g >= 0) == 0) break;
+    if (TIMED) tf[9] += __popcll(__ballot(g >= 0));
     if (TIMED) {
       __builtin_amdgcn_s_waitcnt(0);
       const uint64_t t = __builtin_amdgcn_s_memtime();
@@ -2846,6 +2935,9 @@ __global__ void __launch_bounds__(BS, MINB) k_paths(PathsArgs A) {
         const uint64_t t = __builtin_amdgcn_s_memtime();
         tp[1] += t - tq - cx.mesh_cycles;
         tp[2] += cx.mesh_cycles;
+        tf[10] += cx.mesh_steps;
+        tf[11] += cx.mesh_lane_steps;
+        tf[12] += cx.mesh_walkers;
         tq = t;
       }
       done = true;
@@ -2867,6 +2959,12 @@ __global__ void __launch_bounds__(BS, MINB) k_paths(PathsArgs A) {
           tq = t;
         }
         const int fam = family_of(h.mat, kind, depth, W.max_depth);
+        if (TIMED) {
+          const uint64_t mb = __ballot(fam == FAM_BECK), ms = __ballot(fam == FAM_SPEC),
+                         md = __ballot(fam == FAM_DIFF && S.n_lights > 0);
+          tf[3] += mb != 0; tf[4] += ms != 0; tf[5] += md != 0;
+          tf[6] += __popcll(mb); tf[7] += __popcll(ms); tf[8] += __popcll(md);
+        }
         if (fam == FAM_TERM) {
           C = hit_emitted(S, h.mat, r.d, h.p, h.n, h.u, h.v);
         } else if ((!ALLFAM || fam == FAM_DIFF) && S.n_lights > 0) {
@@ -2886,15 +2984,22 @@ __global__ void __launch_bounds__(BS, MINB) k_paths(PathsArgs A) {
           d_n = h.n;
           diff = pend = true;
           done = false;
+          if (TIMED) tf[2] += __builtin_amdgcn_s_memtime() - tq;
         } else {
           const DMat M = S.mats[h.mat];
           float4 rec;
           bool sp;
           V3 nd;
           float nt;
+          const uint64_t tb = TIMED ? __builtin_amdgcn_s_memtime() : 0;
           if (!ALLFAM || fam == FAM_DIFF) scatter<FAM_DIFF>(S, M, r.d, r.tm, h.p, h.n, h.u, h.v, rng, rec, sp, nd, nt);
-          else if (fam == FAM_BECK) scatter<FAM_BECK>(S, M, r.d, r.tm, h.p, h.n, h.u, h.v, rng, rec, sp, nd, nt);
-          else scatter<FAM_SPEC>(S, M, r.d, r.tm, h.p, h.n, h.u, h.v, rng, rec, sp, nd, nt);
+          else if (fam == FAM_BECK) {
+            scatter<FAM_BECK>(S, M, r.d, r.tm, h.p, h.n, h.u, h.v, rng, rec, sp, nd, nt);
+            if (TIMED) tf[0] += __builtin_amdgcn_s_memtime() - tb;
+          } else {
+            scatter<FAM_SPEC>(S, M, r.d, r.tm, h.p, h.n, h.u, h.v, rng, rec, sp, nd, nt);
+            if (TIMED) tf[1] += __builtin_amdgcn_s_memtime() - tb;
+          }
           if (depth >= W.max_depth || slot >= W.lanes) atomicOr(W.err, 2);
           else rec_store(rec_at(W, depth), rec);
           if (!sp && S.n_lights > 0 && rec.w == 0) ++n_capped;  // the loop reached kMixtureGuard
@@ -2979,6 +3084,7 @@ __global__ void __launch_bounds__(BS, MINB) k_paths(PathsArgs A) {
     atomicAdd(W.counters + 10, (unsigned long long)tp[5]);
     atomicAdd(W.counters + 13, (unsigned long long)tp[6]);
     atomicAdd(W.counters + 14, (unsigned long long)tp[7]);
+    for (int q = 0; q < 13; ++q) atomicAdd(W.counters + 16 + q, (unsigned long long)tf[q]);
   }
   unsigned long long tot = nrays;
   for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);

@@ -52,6 +52,8 @@ int renderer_create_flat(const Flat& F, int device, srr_renderer** out, std::str
   DCamera* cm;
   DObvh* ob;
   DObvhChild* oc;
+  DSGroup* sg;
+  DSGItem* sgi;
   std::vector<DCamera> cam{F.cam};
   RCHK(upload(&objs, F.objs, K));
   RCHK(upload(&xf, F.xforms, K));
@@ -68,6 +70,8 @@ int renderer_create_flat(const Flat& F, int device, srr_renderer** out, std::str
   RCHK(upload(&md, F.media, K));
   RCHK(upload(&ob, F.obvhs, K));
   RCHK(upload(&oc, F.obvh_children, K));
+  RCHK(upload(&sg, F.sgroups, K));
+  RCHK(upload(&sgi, F.sg_items, K));
   RCHK(upload(&mt, F.mats, K));
   RCHK(upload(&tx, F.texs, K));
   RCHK(upload(&im, F.images, K));
@@ -143,6 +147,8 @@ int renderer_create_flat(const Flat& F, int device, srr_renderer** out, std::str
   V.media = md;
   V.obvhs = ob;
   V.obvh_children = oc;
+  V.sgroups = sg;
+  V.sg_items = sgi;
   V.mats = mt;
   V.texs = tx;
   V.images = im;
@@ -329,8 +335,8 @@ static int slot_init(FrameSlot& F, hipStream_t shared_st, std::string& err) {
   }
   RCHK(hipEventCreate(&F.ev_beg));
   RCHK(hipEventCreate(&F.ev_end));
-  RCHK(hipMalloc((void**)&F.ctr, 16 * sizeof(unsigned long long)));
-  RCHK(hipHostMalloc((void**)&F.ctr_host, 16 * sizeof(unsigned long long)));
+  RCHK(hipMalloc((void**)&F.ctr, 32 * sizeof(unsigned long long)));
+  RCHK(hipHostMalloc((void**)&F.ctr_host, 32 * sizeof(unsigned long long)));
   return 0;
 }
 
@@ -416,7 +422,7 @@ static int paths_enqueue(srr_renderer* r, FrameSlot& F, const srr_params* p, boo
     RCHK(e);
     F.sample_cap = win_paths;
   }
-  RCHK(hipMemsetAsync(F.ctr, 0, 16 * sizeof(unsigned long long), st));
+  RCHK(hipMemsetAsync(F.ctr, 0, 32 * sizeof(unsigned long long), st));
   const bool want_sums = (p->flags & SRR_FLAG_SUMS) != 0;
   // per-window HIP events around k_paths, read once the frame is done (no host
   // round trip between windows)
@@ -525,7 +531,7 @@ static int paths_enqueue(srr_renderer* r, FrameSlot& F, const srr_params* p, boo
     else
       launch_finish(acc, d_mean, npix, (int)acc_total, st);
   }
-  RCHK(hipMemcpyAsync(F.ctr_host, F.ctr, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+  RCHK(hipMemcpyAsync(F.ctr_host, F.ctr, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
   RCHK(hipEventRecord(F.ev_end, st));
   F.npix = npix;
   F.paths = npix * p->spp;
@@ -542,13 +548,21 @@ static int paths_finish(srr_renderer* r, FrameSlot& F, const srr_params* p, srr_
     RCHK(hipEventElapsedTime(&ms, F.win_ev[2 * wi], F.win_ev[2 * wi + 1]));
     kernel_ms += ms;
   }
-  unsigned long long ctr[16];
+  unsigned long long ctr[32];
   std::memcpy(ctr, F.ctr_host, sizeof(ctr));
   if (getenv("SRR_PATHS_TIMING") && ctr[9]) {
     const double it = (double)ctr[9];
     fprintf(stderr, "k_paths per wave-iteration (ticks): refill %.0f  world %.0f  mesh %.0f  record %.0f  scatter %.0f  fold %.0f  (%llu wave-iterations)\n",
             ctr[4] / it, ctr[5] / it, ctr[6] / it, ctr[10] / it, (ctr[7] - ctr[10]) / it, ctr[8] / it, ctr[9]);
     fprintf(stderr, "  scatter: mixture loop %.0f ticks, %.2f rounds per wave-iteration\n", ctr[13] / it, ctr[14] / it);
+    auto per = [](unsigned long long a, unsigned long long b) { return b ? (double)a / (double)b : 0.0; };
+    fprintf(stderr, "  families: beck %.0f ticks/it (runs in %.1f %% of its, %.1f lanes/run), spec %.0f (%.1f %%, %.1f), "
+                    "diff set-up %.0f (%.1f %%, %.1f); lanes in a path %.1f of 64\n",
+            ctr[16] / it, 100 * ctr[19] / it, per(ctr[22], ctr[19]), ctr[17] / it, 100 * ctr[20] / it,
+            per(ctr[23], ctr[20]), ctr[18] / it, 100 * ctr[21] / it, per(ctr[24], ctr[21]), ctr[25] / it);
+    fprintf(stderr, "  mesh: longest walk %.1f node steps/it, %.1f lane steps/it over %.1f walking lanes, "
+                    "%.0f ticks per step of the longest walk\n",
+            ctr[26] / it, ctr[27] / it, ctr[28] / it, per(ctr[6], ctr[26]));
   }
 #ifdef SRR_SLOW_RAYS
   if (r->pw_slow) {  // diagnostics build: dump the slow world hits' records (one line per lane, JSON)

@@ -1381,6 +1381,124 @@ static void compact_materials(Flat& F) {
   F.images = std::move(images);
 }
 
+// Sphere runs (device_scene.h DSGroup): every run of >= kSGroupMinRun consecutive
+// world objects that are plain spheres / moving spheres without an instance
+// wrapper becomes one OBJ_SGROUP object over a BVH of their boxes; the spheres'
+// DObjs go to `grouped` (their position in the run is the item's `pos`).
+// SRR_SGROUP=0 keeps the plain list (A/B, parity).
+static std::vector<DObj> group_sphere_runs(const Scene& S, Flat& F, const std::vector<DObj>& in,
+                                           std::vector<DObj>& grouped) {
+  static const bool on = [] {
+    const char* e = getenv("SRR_SGROUP");
+    return !e || atoi(e) != 0;
+  }();
+  // ray times: camera rays carry [time0, time1] (camera.h:57) and keep it through
+  // diffuse bounces; specular rays are built with time 0 (ray.h:10)
+  const double tlo = std::min(0.0, (double)std::min(S.cam.time0, S.cam.time1));
+  const double thi = std::max(0.0, (double)std::max(S.cam.time0, S.cam.time1));
+  auto plain = [&](const DObj& d) {
+    if ((d.kind != OBJ_SPHERE && d.kind != OBJ_MSPHERE) || d.xf_count != 0) return false;
+    const DSphere& sp = F.spheres[d.idx];
+    bool ok = std::isfinite(sp.r);
+    for (int k = 0; k < 3; ++k) ok = ok && std::isfinite(sp.c0[k]) && std::isfinite(sp.c1[k]);
+    if (d.kind == OBJ_MSPHERE) ok = ok && std::isfinite(sp.t0) && std::isfinite(sp.t1) && sp.t1 != sp.t0;
+    return ok;
+  };
+  std::vector<DObj> out;
+  for (size_t i = 0; i < in.size();) {
+    size_t j = i;
+    while (j < in.size() && plain(in[j])) ++j;
+    if (!on || j - i < (size_t)kSGroupMinRun) {
+      out.insert(out.end(), in.begin() + i, in.begin() + (j > i ? j : i + 1));
+      i = j > i ? j : i + 1;
+      continue;
+    }
+    // items and their boxes (the center's whole path over the ray times, widened by
+    // a relative 1e-5 for the float center arithmetic; sgroup_hit adds the per-ray pad)
+    struct It { DSGItem it; double mn[3], mx[3], c[3]; };
+    std::vector<It> items;
+    for (size_t k = i; k < j; ++k) {
+      const DSphere& sp = F.spheres[in[k].idx];
+      It e{};
+      e.it.s = sp;
+      e.it.pos = (int)(k - i);
+      e.it.moving = in[k].kind == OBJ_MSPHERE ? 1 : 0;
+      e.it.obj = (int)grouped.size();  // rebased onto the objs table in flatten()
+      grouped.push_back(in[k]);
+      const double r = std::fabs((double)sp.r);
+      for (int a = 0; a < 3; ++a) {
+        double c0 = sp.c0[a], c1 = c0;
+        if (e.it.moving) {  // center(t) = c0 + ((t - t0) / (t1 - t0)) (c1 - c0), linear in t
+          const double s0 = (tlo - sp.t0) / ((double)sp.t1 - sp.t0), s1 = (thi - sp.t0) / ((double)sp.t1 - sp.t0);
+          c1 = c0 + s1 * ((double)sp.c1[a] - sp.c0[a]);
+          c0 = c0 + s0 * ((double)sp.c1[a] - sp.c0[a]);
+        }
+        const double lo = std::min(c0, c1) - r, hi = std::max(c0, c1) + r;
+        const double w = 1e-5 * (std::max(std::fabs(lo), std::fabs(hi)) + r) + 1e-30;
+        e.mn[a] = lo - w;
+        e.mx[a] = hi + w;
+        e.c[a] = 0.5 * (e.mn[a] + e.mx[a]);
+      }
+      items.push_back(e);
+    }
+    DSGroup g{};
+    g.node_off = (int)(F.nodes.size() / 8);
+    g.item_off = (int)F.sg_items.size();
+    g.n_items = (int)items.size();
+    // top-down median split on the widest centroid axis, leaves of 1-2 spheres, in
+    // preorder with skip links (the threaded format of `nodes`)
+    std::vector<float> nodes;
+    std::function<void(int, int)> build = [&](int lo, int hi) {
+      double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+      double cmn[3] = {INFINITY, INFINITY, INFINITY}, cmx[3] = {-INFINITY, -INFINITY, -INFINITY};
+      for (int k = lo; k < hi; ++k)
+        for (int a = 0; a < 3; ++a) {
+          mn[a] = std::min(mn[a], items[k].mn[a]);
+          mx[a] = std::max(mx[a], items[k].mx[a]);
+          cmn[a] = std::min(cmn[a], items[k].c[a]);
+          cmx[a] = std::max(cmx[a], items[k].c[a]);
+        }
+      const size_t me = nodes.size() / 8;
+      nodes.resize(nodes.size() + 8);
+      // float box rounded outward
+      for (int a = 0; a < 3; ++a) {
+        float fl = (float)mn[a], fh = (float)mx[a];
+        if ((double)fl > mn[a]) fl = std::nextafter(fl, -INFINITY);
+        if ((double)fh < mx[a]) fh = std::nextafter(fh, INFINITY);
+        nodes[8 * me + a] = fl;
+        nodes[8 * me + 4 + a] = fh;
+      }
+      int32_t leaf = -1;
+      if (hi - lo <= 2) {
+        leaf = ((int)F.sg_items.size() << 1) | (hi - lo - 1);
+        for (int k = lo; k < hi; ++k) F.sg_items.push_back(items[k].it);
+      } else {
+        int ax = 0;
+        for (int a = 1; a < 3; ++a)
+          if (cmx[a] - cmn[a] > cmx[ax] - cmn[ax]) ax = a;
+        const int mid = (lo + hi) / 2;
+        std::nth_element(items.begin() + lo, items.begin() + mid, items.begin() + hi,
+                         [ax](const It& x, const It& y) { return x.c[ax] < y.c[ax]; });
+        build(lo, mid);
+        build(mid, hi);
+      }
+      const int32_t skip = g.node_off + (int32_t)(nodes.size() / 8);
+      std::memcpy(&nodes[8 * me + 3], &skip, 4);
+      std::memcpy(&nodes[8 * me + 7], &leaf, 4);
+    };
+    build(0, (int)items.size());
+    g.n_nodes = (int)(nodes.size() / 8);
+    F.nodes.insert(F.nodes.end(), nodes.begin(), nodes.end());
+    F.sgroups.push_back(g);
+    DObj d{};
+    d.kind = OBJ_SGROUP;
+    d.idx = (int)F.sgroups.size() - 1;
+    out.push_back(d);
+    i = j;
+  }
+  return out;
+}
+
 int flatten(const Scene& S, Flat& F, std::string& err) {
   F = Flat();
   if (S.world < 0 || S.lights < 0 || !S.has_camera) {
@@ -1415,13 +1533,18 @@ int flatten(const Scene& S, Flat& F, std::string& err) {
   }
   Flattener fl{S, F, err};
   if (!fl.walk(S.world, {}, fl.world, false)) return -95;
-  F.n_world = (int)fl.world.size();
-  F.objs = fl.world;
+  std::vector<DObj> grouped_objs;  // the spheres moved into sphere groups, kept after every other DObj
+  const std::vector<DObj> world = group_sphere_runs(S, F, fl.world, grouped_objs);
+  F.n_world = (int)world.size();
+  F.objs = world;
   for (DObj d : fl.bound) F.objs.push_back(d);
   for (DMedium& m : F.media) m.bnd_begin += F.n_world;
   const int inner_base = (int)F.objs.size();
   for (DObj d : fl.inner) F.objs.push_back(d);
   for (DObvhChild& c : F.obvh_children) c.obj_begin += inner_base;
+  const int grouped_base = (int)F.objs.size();
+  for (DObj d : grouped_objs) F.objs.push_back(d);
+  for (DSGItem& it : F.sg_items) it.obj += grouped_base;
   for (int k : S.obj[S.lights].kids) {
     if (S.obj[k].kind == H_LIST) {
       err = "nested hitable_list inside the light list is not supported";

@@ -136,6 +136,8 @@ struct Flat {
   std::vector<DMedium> media;
   std::vector<DObvh> obvhs;
   std::vector<DObvhChild> obvh_children;
+  std::vector<DSGroup> sgroups;         // runs of plain spheres behind a BVH (device_scene.h)
+  std::vector<DSGItem> sg_items;
   std::vector<DMat> mats;
   std::vector<DTex> texs;
   std::vector<uint8_t> images;
