@@ -2694,7 +2694,12 @@ SRR_D const PathsArgs* paths_args() { return nullptr; }
 
 template <bool MEDIA, bool ALLFAM, int MINB, bool TIMED = false, bool WL = true, bool QUAD = false, bool CQ = false,
           int BS = kPathsBlock>
-__global__ void __launch_bounds__(BS, MINB) k_paths(PathsArgs A) {
+#ifdef SRR_NUM_VGPR  // register-pressure study builds only: cap k_paths' VGPRs
+#define SRR_PATHS_VGPR_ATTR __attribute__((amdgpu_num_vgpr(SRR_NUM_VGPR)))
+#else
+#define SRR_PATHS_VGPR_ATTR
+#endif
+__global__ void __launch_bounds__(BS, MINB) SRR_PATHS_VGPR_ATTR k_paths(PathsArgs A) {
   static_assert(BS == kPathsBlock || BS == 1024, "block size");
   (void)A;  // read through paths_args()
   // TIMED (diagnostics): per-wave cycles in refill / world hit (mesh part) / record+scatter / fold
