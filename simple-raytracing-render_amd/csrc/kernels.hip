@@ -53,7 +53,11 @@ SRR_D bool sphere_hit(const DSphere& s, bool moving, const Ray& r, float tmin, f
 
 // aarect.h:96-147
 SRR_D bool rect_hit(const DRect& q, const Ray& r, float tmin, float tmax, float& t, float& u, float& v) {
+#ifdef SRR_EXP_FASTRECT  // timing probe only (not the reference's quotient)
+  float tt = (q.k - r.o[q.kax]) * __builtin_amdgcn_rcpf(r.d[q.kax]);
+#else
   float tt = (q.k - r.o[q.kax]) / r.d[q.kax];
+#endif
   if (tt < tmin || tt > tmax) return false;
   float x = r.o[q.a0] + tt * r.d[q.a0];
   float y = r.o[q.a1] + tt * r.d[q.a1];
@@ -260,6 +264,9 @@ struct TraceCtx {
   mutable int mesh_steps = 0;       // node steps of the wave's longest walk
   mutable int mesh_lane_steps = 0;  // node steps summed over the wave's lanes
   mutable int mesh_walkers = 0;     // lanes that took a node step
+  mutable uint64_t leaf_cycles = 0;  // cycles in mesh_hit4's leaf-triangle queue (longest walk's lane)
+  mutable int leaf_passes = 0;       // passes of that queue (the same lane's)
+  mutable uint64_t step_parts[3] = {0, 0, 0};  // node fetch, slab + queue set-up, order + push + pop
 #ifdef SRR_SLOW_RAYS
   mutable int last_steps = 0;  // diagnostics build: node steps | 1 << 30 on overflow, of this lane's last walk
 #endif
@@ -402,7 +409,16 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
   bool overflow = false, deep = false;
   uint32_t nbox = 0, ntri = 0;
   const uint64_t tm_enter = TIMING ? __builtin_amdgcn_s_memtime() : 0;
+  // (step-part stamps; per lane: the longest walk's lane was in every step of the wave)
+  uint64_t ts = TIMING ? __builtin_amdgcn_s_memtime() : 0, sp0 = 0, sp1 = 0, sp2 = 0, slf = 0;
+  int spass = 0;
   for (;;) {
+    if (TIMING) {
+      asm volatile("" ::"v"(node), "v"(sp));
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      sp2 += t - ts;
+      ts = t;
+    }
     float4 LX, LY, LZ, HX, HY, HZ;
     int4 CH;
     if constexpr (Q) {
@@ -434,6 +450,13 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
       CH = *(const int4*)(N + 6);
     }
     nbox += 4;
+    if (TIMING) {  // the node's words are in registers
+      asm volatile("" ::"v"(LX.x), "v"(HZ.w), "v"(CH.x), "v"(CH.w));
+      __builtin_amdgcn_s_waitcnt(0);
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      sp0 += t - ts;
+      ts = t;
+    }
     float near[4];
     bool hit[4];
 #define SRR_CHILD(c, C)                                                                  \
@@ -477,6 +500,10 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
         else q3 = leaf;
       }
       int sub = 0;  // triangle of leaf q0 under test
+      if (TIMING) asm volatile("" ::"v"(q0), "v"(q3), "v"(near[0]), "v"(near[3]));
+      const uint64_t tl_enter = TIMING ? __builtin_amdgcn_s_memtime() : 0;
+      if (TIMING) sp1 += tl_enter - ts;
+      int npass = 0;
 #if SRR_TRIPF
       // software pipelined: the next triangle's vertices are in flight while
       // this one is tested (one L2 / Infinity Cache latency per pass, not two)
@@ -487,6 +514,7 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
       }
 #endif
       while (q0 >= 0) {
+        if (TIMING) ++npass;
         const int ti = (q0 >> 1) + sub;
 #if SRR_TRIPF
         const float4 a = na, b = nb, cc = nc;
@@ -522,6 +550,11 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
           q2 = q3;
           q3 = -1;
         }
+      }
+      if (TIMING) {
+        spass += npass;
+        ts = __builtin_amdgcn_s_memtime();
+        slf += ts - tl_enter;
       }
     } else
 #pragma unroll
@@ -632,6 +665,17 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
     if ((int)__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) atomicAdd(cx.ctr + 67 + min(wmax, 63), 1ull);
   }
   if (TIMING) {
+    sp2 += __builtin_amdgcn_s_memtime() - ts;
+    {  // the parts of the lane with the longest walk (it ran in every step of the wave's loop)
+      int lm = (int)nbox;
+      for (int o = 32; o > 0; o >>= 1) lm = max(lm, __shfl_xor(lm, o));
+      const int src = __ffsll((unsigned long long)__ballot((int)nbox == lm)) - 1;
+      cx.step_parts[0] += (uint64_t)__shfl((unsigned long long)sp0, src);
+      cx.step_parts[1] += (uint64_t)__shfl((unsigned long long)sp1, src);
+      cx.step_parts[2] += (uint64_t)__shfl((unsigned long long)sp2, src);
+      cx.leaf_cycles += (uint64_t)__shfl((unsigned long long)slf, src);
+      cx.leaf_passes += __shfl(spass, src);
+    }
     int st = (int)(nbox / 4), sum = st, walk = st > 0;
     for (int o = 32; o > 0; o >>= 1) {
       st = max(st, __shfl_xor(st, o));
@@ -2455,7 +2499,7 @@ constexpr uint32_t kSpecMark = 0x7f800001u;
 // (attenuation, kSpecMark) with `spec` set.
 template <int F>
 SRR_D void scatter(const SceneView& S, const DMat& M, V3 rdir, float rtime, V3 hpt, V3 nrm, float hu, float hv,
-                   Rng& rng, float4& rec, bool& spec, V3& ndir, float& ntime) {
+                   Rng& rng, float4& rec, bool& spec, V3& ndir, float& ntime, int* attempts = nullptr) {
   ntime = 0.0f;  // ray(a, b) defaults time to 0 (ray.h:10) for specular rays
   if (F == FAM_SPEC) {
     V3 atten;
@@ -2517,6 +2561,7 @@ SRR_D void scatter(const SceneView& S, const DMat& M, V3 rdir, float rtime, V3 h
     if (S.n_lights > 0) {
       (void)drand(rng);  // mixture_pdf ctor (pdf.h:175)
       for (int guard = 0; pdf_val == 0 && guard < kMixtureGuard; ++guard) {
+        if (attempts) ++*attempts;  // (diagnostics)
         if (drand(rng) < 0.5) ndir = lights_random(S, hpt, rng);
         else ndir = bsdf_generate<F == FAM_BECK>(f, rdir, rng);
         pdf_val = 0.5 * lights_pdf(S, hpt, ndir) + 0.5 * bsdf_value<F == FAM_BECK>(f, rdir, ndir);
@@ -2585,6 +2630,9 @@ SRR_D bool shade_one(const SceneView& S, const PathState& P, int p, int max_dept
 // XCD) in L2 for the fold; nontemporal ones stream them to HBM
 #ifndef SRR_REC_NT
 #define SRR_REC_NT 0
+#endif
+#ifndef SRR_FOLD4
+#define SRR_FOLD4 0  // A/B: the fold's record loads four at a time
 #endif
 SRR_D void rec_store(float4* p, float4 v) {
   if (SRR_REC_NT) nts(p, v);
@@ -2708,7 +2756,7 @@ __global__ void __launch_bounds__(BS, MINB) SRR_PATHS_VGPR_ATTR k_paths(PathsArg
   // branches of the per-lane scatter, iterations each branch ran, lanes it ran for;
   // lanes in a path; the longest walk's node steps, all lanes' steps, walking lanes (wave time
   // in the mesh is tp[2])
-  uint64_t tf[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t tf[20] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t it = 0;
   // WL: world tables staged in LDS (they fit in kWorldLdsBytes); otherwise read
   // from global memory (large object lists, e.g. random_scene's ~490 spheres)
@@ -2887,6 +2935,7 @@ __global__ void __launch_bounds__(BS, MINB) SRR_PATHS_VGPR_ATTR k_paths(PathsArg
     // a diffuse bounce with lights: set up here, its mixture loop runs below with
     // the whole wave (coop_mixture), then its record is written
     bool diff = false, pend = false;
+    int natt = 0;  // (TIMED: mixture attempts of this lane's Beckmann scatter)
     DiffSetup ds{};
     V3 d_atten = v3(0.f), d_n = v3(0.f), d_dir = v3(0.f);
     float d_pdf = 0;
@@ -2943,6 +2992,11 @@ __global__ void __launch_bounds__(BS, MINB) SRR_PATHS_VGPR_ATTR k_paths(PathsArg
         tf[10] += cx.mesh_steps;
         tf[11] += cx.mesh_lane_steps;
         tf[12] += cx.mesh_walkers;
+        tf[13] += cx.leaf_cycles;
+        tf[14] += cx.leaf_passes;
+        tf[15] += cx.step_parts[0];
+        tf[16] += cx.step_parts[1];
+        tf[17] += cx.step_parts[2];
         tq = t;
       }
       done = true;
@@ -2999,7 +3053,7 @@ __global__ void __launch_bounds__(BS, MINB) SRR_PATHS_VGPR_ATTR k_paths(PathsArg
           const uint64_t tb = TIMED ? __builtin_amdgcn_s_memtime() : 0;
           if (!ALLFAM || fam == FAM_DIFF) scatter<FAM_DIFF>(S, M, r.d, r.tm, h.p, h.n, h.u, h.v, rng, rec, sp, nd, nt);
           else if (fam == FAM_BECK) {
-            scatter<FAM_BECK>(S, M, r.d, r.tm, h.p, h.n, h.u, h.v, rng, rec, sp, nd, nt);
+            scatter<FAM_BECK>(S, M, r.d, r.tm, h.p, h.n, h.u, h.v, rng, rec, sp, nd, nt, TIMED ? &natt : nullptr);
             if (TIMED) tf[0] += __builtin_amdgcn_s_memtime() - tb;
           } else {
             scatter<FAM_SPEC>(S, M, r.d, r.tm, h.p, h.n, h.u, h.v, rng, rec, sp, nd, nt);
@@ -3013,6 +3067,15 @@ __global__ void __launch_bounds__(BS, MINB) SRR_PATHS_VGPR_ATTR k_paths(PathsArg
           done = false;
         }
       }
+    }
+    if (TIMED) {  // Beckmann mixture attempts: the wave's sum and its slowest lane's
+      int sum = natt, mx = natt;
+      for (int o = 32; o > 0; o >>= 1) {
+        sum += __shfl_xor(sum, o);
+        mx = max(mx, __shfl_xor(mx, o));
+      }
+      tf[18] += sum;
+      tf[19] += mx;
     }
     if (__ballot(pend)) {
       const SceneView S = view();
@@ -3057,12 +3120,30 @@ __global__ void __launch_bounds__(BS, MINB) SRR_PATHS_VGPR_ATTR k_paths(PathsArg
       }
       if (done) {
         // fold the bounces back to front (Raytracing_n.cpp:69, :94), as finish_path
+#if SRR_FOLD4
+        // the last four records' loads issued together (one L2 round trip, not one
+        // per bounce), then folded in the same order
+        int k = depth - 1;
+        for (; k >= 0; k -= 4) {
+          float4 a[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) a[j] = k - j >= 0 ? rec_load(rec_at(W, k - j)) : make_float4(0, 0, 0, 0);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (k - j < 0) break;
+            const V3 av = v3(a[j].x, a[j].y, a[j].z);
+            if (__float_as_uint(a[j].w) == kSpecMark) C = av * C;  // specular: attenuation * color
+            else C = v3(0.f) + (av * C) / a[j].w;
+          }
+        }
+#else
         for (int k = depth - 1; k >= 0; --k) {
           const float4 a = rec_load(rec_at(W, k));
           const V3 av = v3(a.x, a.y, a.z);
           if (__float_as_uint(a.w) == kSpecMark) C = av * C;  // specular: attenuation * color
           else C = v3(0.f) + (av * C) / a.w;
         }
+#endif
         if (W.raw) {  // kept paths: [pixel][sample of the frame]
           const size_t kq = (size_t)(g / W.spp_w) * W.keep_spp + W.keep_s0 + (size_t)(g % W.spp_w);
           W.raw[3 * kq] = C.x;
@@ -3089,7 +3170,7 @@ __global__ void __launch_bounds__(BS, MINB) SRR_PATHS_VGPR_ATTR k_paths(PathsArg
     atomicAdd(W.counters + 10, (unsigned long long)tp[5]);
     atomicAdd(W.counters + 13, (unsigned long long)tp[6]);
     atomicAdd(W.counters + 14, (unsigned long long)tp[7]);
-    for (int q = 0; q < 13; ++q) atomicAdd(W.counters + 16 + q, (unsigned long long)tf[q]);
+    for (int q = 0; q < 20; ++q) atomicAdd(W.counters + 16 + q, (unsigned long long)tf[q]);
   }
   unsigned long long tot = nrays;
   for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);

@@ -13,6 +13,7 @@
 
 namespace srr {
 
+constexpr int kCtrWords = 40;  // FrameSlot::ctr: world rays, cursor, error, overflow and diagnostics counters
 constexpr int kVisitWords = 3 + 2 * 64;  // SRR_FLAG_COUNT_VISITS: sums + two histograms
 
 #define RCHK(x)                                                        \
@@ -335,8 +336,8 @@ static int slot_init(FrameSlot& F, hipStream_t shared_st, std::string& err) {
   }
   RCHK(hipEventCreate(&F.ev_beg));
   RCHK(hipEventCreate(&F.ev_end));
-  RCHK(hipMalloc((void**)&F.ctr, 32 * sizeof(unsigned long long)));
-  RCHK(hipHostMalloc((void**)&F.ctr_host, 32 * sizeof(unsigned long long)));
+  RCHK(hipMalloc((void**)&F.ctr, kCtrWords * sizeof(unsigned long long)));
+  RCHK(hipHostMalloc((void**)&F.ctr_host, kCtrWords * sizeof(unsigned long long)));
   return 0;
 }
 
@@ -422,7 +423,7 @@ static int paths_enqueue(srr_renderer* r, FrameSlot& F, const srr_params* p, boo
     RCHK(e);
     F.sample_cap = win_paths;
   }
-  RCHK(hipMemsetAsync(F.ctr, 0, 32 * sizeof(unsigned long long), st));
+  RCHK(hipMemsetAsync(F.ctr, 0, kCtrWords * sizeof(unsigned long long), st));
   const bool want_sums = (p->flags & SRR_FLAG_SUMS) != 0;
   // per-window HIP events around k_paths, read once the frame is done (no host
   // round trip between windows)
@@ -531,7 +532,7 @@ static int paths_enqueue(srr_renderer* r, FrameSlot& F, const srr_params* p, boo
     else
       launch_finish(acc, d_mean, npix, (int)acc_total, st);
   }
-  RCHK(hipMemcpyAsync(F.ctr_host, F.ctr, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+  RCHK(hipMemcpyAsync(F.ctr_host, F.ctr, kCtrWords * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
   RCHK(hipEventRecord(F.ev_end, st));
   F.npix = npix;
   F.paths = npix * p->spp;
@@ -548,7 +549,7 @@ static int paths_finish(srr_renderer* r, FrameSlot& F, const srr_params* p, srr_
     RCHK(hipEventElapsedTime(&ms, F.win_ev[2 * wi], F.win_ev[2 * wi + 1]));
     kernel_ms += ms;
   }
-  unsigned long long ctr[32];
+  unsigned long long ctr[kCtrWords];
   std::memcpy(ctr, F.ctr_host, sizeof(ctr));
   if (getenv("SRR_PATHS_TIMING") && ctr[9]) {
     const double it = (double)ctr[9];
@@ -563,6 +564,12 @@ static int paths_finish(srr_renderer* r, FrameSlot& F, const srr_params* p, srr_
     fprintf(stderr, "  mesh: longest walk %.1f node steps/it, %.1f lane steps/it over %.1f walking lanes, "
                     "%.0f ticks per step of the longest walk\n",
             ctr[26] / it, ctr[27] / it, ctr[28] / it, per(ctr[6], ctr[26]));
+    fprintf(stderr, "  mesh leaf queue: %.0f ticks/it, %.1f passes/it (%.0f ticks per pass)\n", ctr[29] / it,
+            ctr[30] / it, per(ctr[29], ctr[30]));
+    fprintf(stderr, "  mesh step parts (ticks/it): node fetch %.0f  slab + queue %.0f  order + push + pop %.0f\n",
+            ctr[31] / it, ctr[32] / it, ctr[33] / it);
+    fprintf(stderr, "  beckmann mixture: %.2f attempts per Beckmann scatter, %.2f for the wave's slowest lane per run\n",
+            per(ctr[34], ctr[22]), per(ctr[35], ctr[19]));
   }
 #ifdef SRR_SLOW_RAYS
   if (r->pw_slow) {  // diagnostics build: dump the slow world hits' records (one line per lane, JSON)

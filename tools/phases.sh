@@ -11,5 +11,5 @@ declare -A ARGS=([c1]="--scene s1 --steps 3" [c2]="" [c3]="--scene s3" [c3m]="--
 for c in ${@:-c2 c3 c4 c5 c4r}; do
   SRR_LIB=$L/libsrr_diag.so SRR_PATHS_TIMING=1 timeout -k 10 300 python bench.py --no-cpu-baseline --no-pipeline \
     --warmup 0 --steps 1 ${ARGS[$c]} > gpurun_out/$TAG.$c.log 2>&1 || { echo "$c failed"; tail -3 gpurun_out/$TAG.$c.log; exit 1; }
-  echo "== $c"; grep -h "per wave-iteration\|mixture loop\|families:\|  mesh:" gpurun_out/$TAG.$c.log | tail -4
+  echo "== $c"; grep -h "per wave-iteration\|mixture loop\|families:\|  mesh\|  beckmann" gpurun_out/$TAG.$c.log | tail -7
 done
