@@ -2632,7 +2632,7 @@ SRR_D bool shade_one(const SceneView& S, const PathState& P, int p, int max_dept
 #define SRR_REC_NT 0
 #endif
 #ifndef SRR_FOLD4
-#define SRR_FOLD4 0  // A/B: the fold's record loads four at a time
+#define SRR_FOLD4 1  // the fold's record loads four at a time (A/B: -DSRR_FOLD4=0)
 #endif
 SRR_D void rec_store(float4* p, float4 v) {
   if (SRR_REC_NT) nts(p, v);
