@@ -378,6 +378,9 @@ constexpr bool LEAFQ = SRR_LEAFQ != 0;  // mesh_hit4's leaf-triangle queue (A/B:
 #ifndef SRR_TRIPF
 #define SRR_TRIPF 1
 #endif
+#ifndef SRR_LEAFPAIR
+#define SRR_LEAFPAIR 1  // one leaf (both triangles) per pass of the leaf queue (A/B: -DSRR_LEAFPAIR=0)
+#endif
 
 template <bool PRUNE, bool TIMING = false, bool Q = false, int STRIDE = kTraceBlock>
 SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmin, float tmax, bool is_medium,
@@ -504,6 +507,43 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
       const uint64_t tl_enter = TIMING ? __builtin_amdgcn_s_memtime() : 0;
       if (TIMING) sp1 += tl_enter - ts;
       int npass = 0;
+#if SRR_LEAFPAIR
+      // one pass per leaf: both its triangles' vertices are loaded together (a
+      // one-triangle leaf loads its triangle twice, from L1) and tested, so a pass
+      // waits for one round trip per leaf, not one per triangle
+      (void)sub;
+      while (q0 >= 0) {
+        if (TIMING) ++npass;
+        const int t0 = q0 >> 1;
+        const bool two = (q0 & 1) != 0;
+        const float4* tp = S.tri_pos + kTriStride * (size_t)t0;
+        const float4* tq = tp + (two ? kTriStride : 0);
+        const float4 a0 = tp[0], b0 = tp[1], c0 = tp[2];
+        const float4 a1 = tq[0], b1 = tq[1], c1 = tq[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          if (j == 1 && !two) break;
+          const float4 a = j ? a1 : a0, b = j ? b1 : b0, cc = j ? c1 : c0;
+          const int ti = t0 + j;
+          const V3 p0 = v3(a.x, a.y, a.z), p1 = v3(b.x, b.y, b.z), p2 = v3(cc.x, cc.y, cc.z);
+          float t, u, v;
+          bool h = tri_hit(p0, p1, p2, true, r.o, dir, t, u, v);
+          if (!h && is_medium) h = tri_hit(p0, p1, p2, false, r.o, dir, t, u, v);
+          if (h && (!found || wins(t, ti, best_t, best_i))) {
+            found = true;
+            best_t = t;
+            best_i = ti;
+          }
+        }
+        // shrink only with ordered compares: a NaN bound (the reference passes
+        // every box then) or a NaN best keeps the bound as it is
+        if (PRUNE && found && best_t * to_param < bound) bound = best_t * to_param;
+        q0 = q1;
+        q1 = q2;
+        q2 = q3;
+        q3 = -1;
+      }
+#else
 #if SRR_TRIPF
       // software pipelined: the next triangle's vertices are in flight while
       // this one is tested (one L2 / Infinity Cache latency per pass, not two)
@@ -551,6 +591,7 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
           q3 = -1;
         }
       }
+#endif
       if (TIMING) {
         spass += npass;
         ts = __builtin_amdgcn_s_memtime();
