@@ -378,6 +378,9 @@ constexpr bool LEAFQ = SRR_LEAFQ != 0;  // mesh_hit4's leaf-triangle queue (A/B:
 #ifndef SRR_TRIPF
 #define SRR_TRIPF 1
 #endif
+#ifndef SRR_TOPREG
+#define SRR_TOPREG 1  // the stack's top entry kept in registers (A/B: -DSRR_TOPREG=0)
+#endif
 #ifndef SRR_LEAFPAIR
 #define SRR_LEAFPAIR 1  // one leaf (both triangles) per pass of the leaf queue (A/B: -DSRR_LEAFPAIR=0)
 #endif
@@ -415,6 +418,10 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
   // (step-part stamps; per lane: the longest walk's lane was in every step of the wave)
   uint64_t ts = TIMING ? __builtin_amdgcn_s_memtime() : 0, sp0 = 0, sp1 = 0, sp2 = 0, slf = 0;
   int spass = 0;
+#if SRR_TOPREG
+  int top_n = -1;
+  float top_t = 0.f;
+#endif
   for (;;) {
     if (TIMING) {
       asm volatile("" ::"v"(node), "v"(sp));
@@ -656,6 +663,51 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
   }
     SRR_CSWAP(0, 1) SRR_CSWAP(2, 3) SRR_CSWAP(0, 2) SRR_CSWAP(1, 3) SRR_CSWAP(1, 2)
 #undef SRR_CSWAP
+#if SRR_TOPREG
+    // the stack's top entry is also kept in registers (top_n, top_t: entry sp - 1
+    // whenever sp > 0), so a pop has its node at once and reads the entry below it
+    // from LDS while the next step runs
+    if (kn[0] >= 0) {
+      node = kn[0];
+#pragma unroll
+      for (int c = 3; c >= 1; --c) {
+        if (kn[c] < 0) continue;
+        if (sp < cx.st_cap) {
+          cx.st_node[sp * STRIDE] = kn[c];
+          cx.st_t[sp * STRIDE] = kt[c];
+          ++sp;
+          top_n = kn[c];
+          top_t = kt[c];
+        } else if (sp < cx.st_cap + cx.gst_cap) {
+          cx.gst[(size_t)(sp - cx.st_cap) * cx.gst_stride + cx.slot] = make_int2(kn[c], __float_as_int(kt[c]));
+          ++sp;
+          deep = true;
+          top_n = kn[c];
+          top_t = kt[c];
+        } else {
+          overflow = true;
+        }
+      }
+      continue;
+    }
+    int nx = -1;
+    while (sp > 0) {
+      --sp;
+      const int cand = top_n;
+      const float ct = top_t;
+      if (sp > 0) {  // the new top
+        if (sp - 1 < cx.st_cap) {
+          top_n = cx.st_node[(sp - 1) * STRIDE];
+          top_t = cx.st_t[(sp - 1) * STRIDE];
+        } else {
+          const int2 e = cx.gst[(size_t)(sp - 1 - cx.st_cap) * cx.gst_stride + cx.slot];
+          top_n = e.x;
+          top_t = __int_as_float(e.y);
+        }
+      }
+      if (!(PRUNE && ct > bound)) { nx = cand; break; }
+    }
+#else
     if (kn[0] >= 0) {
       node = kn[0];
 #pragma unroll
@@ -691,6 +743,7 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
       }
       if (!(PRUNE && ct > bound)) { nx = cand; break; }
     }
+#endif
     if (nx < 0) break;
     node = nx;
   }
