@@ -350,13 +350,28 @@ SRR_D void mesh_scan_nan(const SceneView& S, const DMesh& m, const Ray& r, bool 
   }
 }
 
+// A slab's running entry / exit over the axes, from -inf / +inf (never NaN): the
+// reference's `t0 > tmin ? t0 : tmin` keeps tmin for a NaN t0, as fmaxf does (and a
+// +-0 difference compares equal everywhere the entry is used), so with SRR_FMINMAX the
+// compare + select pairs become single v_max_f32 / v_min_f32
+#ifndef SRR_FMINMAX
+#define SRR_FMINMAX 1  // (A/B: -DSRR_FMINMAX=0)
+#endif
+#if SRR_FMINMAX
+#define SRR_SMAX(n, acc) fmaxf((n), (acc))
+#define SRR_SMIN(f, acc) fminf((f), (acc))
+#else
+#define SRR_SMAX(n, acc) ((n) > (acc) ? (n) : (acc))
+#define SRR_SMIN(f, acc) ((f) < (acc) ? (f) : (acc))
+#endif
+
 // one axis of a slab test on the whole line (as SRR_CHILD's): entry / exit
 SRR_D void slab_axis(float L, float H, float O, float I, float& lo, float& hi) {
   const float t0 = (L - O) * I, t1 = (H - O) * I;
   const bool sw = I < 0.0f;
   const float n = sw ? t1 : t0, f = sw ? t0 : t1;
-  lo = n > lo ? n : lo;
-  hi = f < hi ? f : hi;
+  lo = SRR_SMAX(n, lo);
+  hi = SRR_SMIN(f, hi);
 }
 
 // A compressed node's box bound (device_scene.h kNode4qWords): o + q * s with
@@ -483,8 +498,8 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
     float t0 = (L - O) * I, t1 = (H - O) * I;        \
     bool sw = I < 0.0f;                              \
     float n_ = sw ? t1 : t0, f_ = sw ? t0 : t1;      \
-    lo_ = n_ > lo_ ? n_ : lo_;                       \
-    hi_ = f_ < hi_ ? f_ : hi_;                       \
+    lo_ = SRR_SMAX(n_, lo_);                         \
+    hi_ = SRR_SMIN(f_, hi_);                         \
   }
     SRR_CHILD(0, x) SRR_CHILD(1, y) SRR_CHILD(2, z) SRR_CHILD(3, w)
 #undef SRR_SLAB_AX
@@ -915,8 +930,8 @@ SRR_D bool mesh_hit4_quad(const SceneView& S, const DMesh& m, const Ray& r, floa
     float t0 = (L - O) * I, t1 = (H - O) * I;    \
     bool sw = I < 0.0f;                          \
     float n_ = sw ? t1 : t0, f_ = sw ? t0 : t1;  \
-    lo_ = n_ > lo_ ? n_ : lo_;                   \
-    hi_ = f_ < hi_ ? f_ : hi_;                   \
+    lo_ = SRR_SMAX(n_, lo_);                     \
+    hi_ = SRR_SMIN(f_, hi_);                     \
   }
         SRR_QAX(lx, hx, o.x, iv.x) SRR_QAX(ly, hy, o.y, iv.y) SRR_QAX(lz, hz, o.z, iv.z)
 #undef SRR_QAX
@@ -1186,8 +1201,8 @@ SRR_D bool sgroup_hit(const SceneView& S, const DSGroup& g, const Ray& r, float 
     const float t1 = (hi.A + pad - r.o.A) * inv.A;        \
     const bool sw = inv.A < 0.0f;                         \
     const float n_ = sw ? t1 : t0, f_ = sw ? t0 : t1;     \
-    tn = n_ > tn ? n_ : tn;                               \
-    tf = f_ < tf ? f_ : tf;                               \
+    tn = SRR_SMAX(n_, tn);                                \
+    tf = SRR_SMIN(f_, tf);                                \
   }
     SRR_AX(x) SRR_AX(y) SRR_AX(z)
 #undef SRR_AX
