@@ -365,6 +365,23 @@ SRR_D void mesh_scan_nan(const SceneView& S, const DMesh& m, const Ray& r, bool 
 #define SRR_SMIN(f, acc) ((f) < (acc) ? (f) : (acc))
 #endif
 
+// SRR_SLIM: in mesh_hit4's walk (whose lanes never carry a NaN bound: those took
+// the fold over all triangles), a child's [max(entry, tmin), min(exit, tmax)] by
+// fmaxf / fminf, and the child sort's swap test on the entries alone (a child not
+// taken has entry +inf and node -1; a taken child's entry is finite or -inf)
+#ifndef SRR_SLIM
+#define SRR_SLIM 1  // (A/B: -DSRR_SLIM=0)
+#endif
+#if SRR_SLIM
+#define SRR_CMAX(x, t) fmaxf((x), (t))
+#define SRR_CMIN(x, t) fminf((x), (t))
+#define SRR_CSWAP_IF(a, b) (kt[b] < kt[a])
+#else
+#define SRR_CMAX(x, t) ((x) > (t) ? (x) : (t))
+#define SRR_CMIN(x, t) ((x) < (t) ? (x) : (t))
+#define SRR_CSWAP_IF(a, b) (kn[b] >= 0 && (kn[a] < 0 || kt[b] < kt[a]))
+#endif
+
 // one axis of a slab test on the whole line (as SRR_CHILD's): entry / exit
 SRR_D void slab_axis(float L, float H, float O, float I, float& lo, float& hi) {
   const float t0 = (L - O) * I, t1 = (H - O) * I;
@@ -490,7 +507,7 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
     SRR_SLAB_AX(LX.C, HX.C, r.o.x, inv.x) SRR_SLAB_AX(LY.C, HY.C, r.o.y, inv.y)          \
     SRR_SLAB_AX(LZ.C, HZ.C, r.o.z, inv.z)                                                \
     near[c] = lo_;                                                                       \
-    const float a_ = lo_ > tmin ? lo_ : tmin, b_ = hi_ < tmax ? hi_ : tmax;              \
+    const float a_ = SRR_CMAX(lo_, tmin), b_ = SRR_CMIN(hi_, tmax);                      \
     hit[c] = !(b_ <= a_) && !(PRUNE && lo_ > bound);                                     \
   }
 #define SRR_SLAB_AX(L, H, O, I)                      \
@@ -672,7 +689,7 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
       kn[c] = take ? ch[c] : -1;
     }
 #define SRR_CSWAP(a, b)                                          \
-  if (kn[b] >= 0 && (kn[a] < 0 || kt[b] < kt[a])) {              \
+  if (SRR_CSWAP_IF(a, b)) {                                      \
     float tt_ = kt[a]; kt[a] = kt[b]; kt[b] = tt_;               \
     int nn_ = kn[a]; kn[a] = kn[b]; kn[b] = nn_;                 \
   }
