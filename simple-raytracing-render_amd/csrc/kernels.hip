@@ -51,6 +51,23 @@ SRR_D bool sphere_hit(const DSphere& s, bool moving, const Ray& r, float tmin, f
   return false;
 }
 
+// rect_hit with the plane axis a compile-time constant (xy: 2, xz: 1, yz: 0), for the
+// world list's hit test (t only), dispatched on the rect's (uniform) axis
+template <int KAX>
+SRR_D bool rect_hit_t(const DRect& q, const Ray& r, float tmin, float tmax, float& t) {
+  constexpr int A0 = KAX == 0 ? 1 : 0, A1 = KAX == 2 ? 1 : 2;
+  const float tt = (q.k - r.o[KAX]) / r.d[KAX];
+  if (tt < tmin || tt > tmax) return false;
+  const float x = r.o[A0] + tt * r.d[A0];
+  const float y = r.o[A1] + tt * r.d[A1];
+  if (x < q.lo0 || x > q.hi0 || y < q.lo1 || y > q.hi1) return false;
+  t = tt;
+  return true;
+}
+
+#ifndef SRR_RECTAX
+#define SRR_RECTAX 1  // rect tests specialised on the plane axis (A/B: -DSRR_RECTAX=0)
+#endif
 // aarect.h:96-147
 SRR_D bool rect_hit(const DRect& q, const Ray& r, float tmin, float tmax, float& t, float& u, float& v) {
 #ifdef SRR_EXP_FASTRECT  // timing probe only (not the reference's quotient)
@@ -1125,8 +1142,17 @@ SRR_D bool prim_hit(const SceneView& S, const DObj& ob, const Ray& lr, float tmi
     case OBJ_MSPHERE:
       return sphere_hit(maybe_uni<U>(wload<TR>(S.spheres, ob.idx)), ob.kind == OBJ_MSPHERE, lr, tmin, tmax, t);
     case OBJ_RECT: {
+#if SRR_RECTAX
+      const DRect q = maybe_uni<U>(wload<TR>(S.rects, ob.idx));
+      switch (q.kax) {
+        case 0: return rect_hit_t<0>(q, lr, tmin, tmax, t);
+        case 1: return rect_hit_t<1>(q, lr, tmin, tmax, t);
+        default: return rect_hit_t<2>(q, lr, tmin, tmax, t);
+      }
+#else
       float u, v;
       return rect_hit(maybe_uni<U>(wload<TR>(S.rects, ob.idx)), lr, tmin, tmax, t, u, v);
+#endif
     }
     case OBJ_TRI: {
       const DStandaloneTri T = maybe_uni<U>(wload<TR>(S.stris, ob.idx));
@@ -1826,8 +1852,13 @@ SRR_D float light_pdf_one(const SceneView& S, const DLight& L, V3 o, V3 v) {
   Ray r{o, v, 0.0f};
   if (L.kind == LIGHT_XZRECT) {  // aarect.h:45-55
     const DRect& q = S.rects[L.idx];
-    float t, u, vv;
+    float t;
+#if SRR_RECTAX
+    if (rect_hit_t<1>(q, r, 0.001f, FLT_MAX, t)) {  // an xz_rect light (kax 1)
+#else
+    float u, vv;
     if (rect_hit(q, r, 0.001f, FLT_MAX, t, u, vv)) {
+#endif
       float area = (q.hi0 - q.lo0) * (q.hi1 - q.lo1);
       float distance_square = t * t * squared_length(v);
       float cosine = fabsf(v.y / length(v));  // dot(v, (0,1,0)) / |v|
