@@ -1084,6 +1084,32 @@ SRR_D bool mesh_hit4_quad(const SceneView& S, const DMesh& m, const Ray& r, floa
   return found_me;
 }
 
+#ifndef SRR_XFAX
+#define SRR_XFAX 1  // rotations, record rects and light corners specialised on their axis (A/B: -DSRR_XFAX=0)
+#endif
+template <int IA>  // rotate_y (IA 0) / rotate_x (IA 1), the ray going in: the arithmetic of chain_in's generic branch
+SRR_D void rot_in(const DXform& x, Ray& r) {
+  const float s = x.a, c = x.b;
+  V3 o = r.o, d = r.d;
+  o.set(IA, c * r.o[IA] - s * r.o.z);
+  o.z = s * r.o[IA] + c * r.o.z;
+  d.set(IA, c * r.d[IA] - s * r.d.z);
+  d.z = s * r.d[IA] + c * r.d.z;
+  r.o = o;
+  r.d = d;
+}
+template <int IA>  // ...and the record coming out
+SRR_D void rot_out(const DXform& x, V3& p, V3& n) {
+  const float s = x.a, c = x.b;
+  V3 pp = p, nn = n;
+  pp.set(IA, c * p[IA] + s * p.z);
+  pp.z = -s * p[IA] + c * p.z;
+  nn.set(IA, c * n[IA] + s * n.z);
+  nn.z = -s * n[IA] + c * n.z;
+  p = pp;
+  n = nn;
+}
+
 // Instance chain (outermost first): the ray going in (hitable.h:44-52, 109-116,
 // 180-188; flip leaves the ray alone)
 template <int TR = 0, bool U = false>
@@ -1092,6 +1118,10 @@ SRR_D Ray chain_in(const SceneView& S, const DObj& ob, Ray r) {
   for (int k = 0; k < n; ++k) {
     DXform x = maybe_uni<U>(wload<TR>(S.xforms, ob.xf_begin + k));
     if (x.kind == XF_TRANSLATE) r.o = r.o - v3(x.a, x.b, x.c);
+#if SRR_XFAX  // the rotation's axis a compile-time constant in each branch (no run-time indexing)
+    else if (x.kind == XF_ROTY) rot_in<0>(x, r);
+    else if (x.kind == XF_ROTX) rot_in<1>(x, r);
+#else
     else if (x.kind == XF_ROTY || x.kind == XF_ROTX) {
       int ia = x.kind == XF_ROTY ? 0 : 1;
       float s = x.a, c = x.b;
@@ -1103,6 +1133,7 @@ SRR_D Ray chain_in(const SceneView& S, const DObj& ob, Ray r) {
       r.o = o;
       r.d = d;
     }
+#endif
   }
   return r;
 }
@@ -1112,6 +1143,10 @@ SRR_D void chain_out(const SceneView& S, const DObj& ob, V3& p, V3& n) {
   for (int k = (ob.xf_count & kXfCountMask) - 1; k >= 0; --k) {
     DXform x = S.xforms[ob.xf_begin + k];
     if (x.kind == XF_TRANSLATE) p = p + v3(x.a, x.b, x.c);
+#if SRR_XFAX
+    else if (x.kind == XF_ROTY) rot_out<0>(x, p, n);
+    else rot_out<1>(x, p, n);
+#else
     else {
       int ia = x.kind == XF_ROTY ? 0 : 1;
       float s = x.a, c = x.b;
@@ -1123,6 +1158,7 @@ SRR_D void chain_out(const SceneView& S, const DObj& ob, V3& p, V3& n) {
       p = pp;
       n = nn;
     }
+#endif
   }
   if (ob.xf_count & kXfFlipBit) n = -n;  // flip_normals (aarect.h:149-171), exact in any order
 }
@@ -1457,6 +1493,22 @@ struct HitRec {
   int mat;
 };
 
+#if SRR_XFAX
+// prim_record's rect branch with the plane axis a compile-time constant: u, v by
+// rect_hit's arithmetic (aarect.h:96-147), the normal along the axis
+template <int KAX>
+SRR_D void rect_rec(const DRect& q, const Ray& r, HitRec& h) {
+  constexpr int A0 = KAX == 0 ? 1 : 0, A1 = KAX == 2 ? 1 : 2;
+  const float tt = (q.k - r.o[KAX]) / r.d[KAX];
+  const float x = r.o[A0] + tt * r.d[A0];
+  const float y = r.o[A1] + tt * r.d[A1];
+  h.u = (x - q.lo0) / (q.hi0 - q.lo0);
+  h.v = (y - q.lo1) / (q.hi1 - q.lo1);
+  h.n = v3(0.f);
+  h.n.set(KAX, 1.f);
+}
+#endif
+
 SRR_D void sphere_uv(V3 p, float& u, float& v) {  // hitable.h:10-15
   float phi = ratan2(p.z, p.x);
   float theta = rasin(p.y);
@@ -1480,11 +1532,19 @@ SRR_D void prim_record(const SceneView& S, const DObj& ob, const Ray& lr, float 
     }
     case OBJ_RECT: {
       const DRect& q = S.rects[ob.idx];
+#if SRR_XFAX
+      switch (q.kax) {
+        case 0: rect_rec<0>(q, lr, h); break;
+        case 1: rect_rec<1>(q, lr, h); break;
+        default: rect_rec<2>(q, lr, h); break;
+      }
+#else
       float tt;
       rect_hit(q, lr, -FLT_MAX, FLT_MAX, tt, h.u, h.v);
-      h.p = lr.at(t);
       h.n = v3(0.f);
       h.n.set(q.kax, 1.f);
+#endif
+      h.p = lr.at(t);
       h.mat = q.mat;
       break;
     }
@@ -2337,14 +2397,22 @@ SRR_D bool bsdf_dead(const SceneView& S, const Bsdf& f, V3 p) {
     const DLight L = S.lights[k];
     if (L.kind == LIGHT_XZRECT) {
       const DRect q = S.rects[L.idx];
+#if SRR_XFAX  // an xz_rect light: kax 1, a0 0, a1 2
+      if (!(q.k != p.y)) return false;  // the hit point in the light's plane
+#else
       if (!(q.k != p[q.kax])) return false;  // the hit point in the light's plane
+#endif
       const float m = 1e-3f * (ps + fmaxf(fmaxf(fmaxf(fabsf(q.lo0), fabsf(q.hi0)), fmaxf(fabsf(q.lo1), fabsf(q.hi1))),
                                           fabsf(q.k)));
       for (int c = 0; c < 4; ++c) {
+#if SRR_XFAX
+        const V3 v = v3((c & 1) ? q.hi0 : q.lo0, q.k, (c & 2) ? q.hi1 : q.lo1);
+#else
         V3 v = v3(0.f);
         v.set(q.kax, q.k);
         v.set(q.a0, (c & 1) ? q.hi0 : q.lo0);
         v.set(q.a1, (c & 2) ? q.hi1 : q.lo1);
+#endif
         if (!light_point_far(v, p, w, sgn, m)) return false;
       }
     } else if (L.kind == LIGHT_SPHERE) {
