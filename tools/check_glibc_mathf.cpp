@@ -55,6 +55,8 @@ int main() {
   exhaustive("logf", [](float x) { return logf_(x); }, [](float x) { return ::logf(x); });
   exhaustive("sinf", [](float x) { return sinf_(x); }, [](float x) { return ::sinf(x); });
   exhaustive("cosf", [](float x) { return cosf_(x); }, [](float x) { return ::cosf(x); });
+  exhaustive("sincosf (sine)", [](float x) { float s, c; sincosf_(x, s, c); return s; }, [](float x) { return ::sinf(x); });
+  exhaustive("sincosf (cosine)", [](float x) { float s, c; sincosf_(x, s, c); return c; }, [](float x) { return ::cosf(x); });
   exhaustive("acosf", [](float x) { return acosf_(x); }, [](float x) { return ::acosf(x); });
   exhaustive("asinf", [](float x) { return asinf_(x); }, [](float x) { return ::asinf(x); });
   exhaustive("atanf", [](float x) { return atanf_(x); }, [](float x) { return ::atanf(x); });
