@@ -249,6 +249,37 @@ GM_FN float cosf_(float y) {
   return y - y;  // inf / nan
 }
 
+// sinf_(y) and cosf_(y) together, each bit for bit the function's own result: one
+// range reduction and, where |y| < 120, both polynomials evaluated once and picked per
+// quadrant without a branch (sinf_poly's parity test splits a wave into both paths)
+GM_FN void sincosf_(float y, float& so, float& co) {
+  const uint32_t a = top12(y) & 0x7ff;
+  if (a < (top12(0x1.921fb6p-1f) & 0x7ff) || !(a < (top12(120.0f) & 0x7ff))) {
+    so = sinf_(y);
+    co = cosf_(y);
+    return;
+  }
+  int n;
+  const double x = reduce_fast((double)y, n);
+  const double xs = x * quadrant_sign(n & 3), x2 = x * x;
+  // sinf_poly's two branches on (xs, x2) with the same sign flag
+  const double x3 = xs * x2;
+  const double s1 = GM_FMA(x2, kSc_s3, kSc_s2);
+  const double x7 = x3 * x2;
+  const double sv = GM_FMA(x3, kSc_s1, xs);
+  const float S = (float)GM_FMA(x7, s1, sv);
+  const double x4 = x2 * x2;
+  const double c2 = GM_FMA(x2, kSc_c4, kSc_c3);
+  const double c1 = GM_FMA(x2, kSc_c1, kSc_c0);
+  const double x6 = x4 * x2;
+  const double cv = GM_FMA(x4, kSc_c2, c1);
+  const float r = (float)GM_FMA(x6, c2, cv);
+  const float C = (n & 2) ? -r : r;
+  const bool even = (n & 1) == 0;
+  so = even ? S : C;
+  co = even ? C : S;
+}
+
 // e_acosf.c (fdlibm's float acos, which glibc 2.35 keeps): float arithmetic,
 // rational approximation on z = x^2 or z = (1 -+ x)/2
 GM_FN float acosf_(float x) {

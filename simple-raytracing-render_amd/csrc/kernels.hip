@@ -1876,14 +1876,24 @@ SRR_D V3 beckmann_sample_wh(const Beck& d, V3 wo, float u1, float u2) {  // :12-
   return wh;
 }
 
+#ifndef SRR_SINCOS
+#define SRR_SINCOS 0  // A/B: random_cosine_direction's sine and cosine from one sincosf_
+#endif
 // pdf.h:10-18
 SRR_D V3 random_cosine_direction(Rng& rng) {
   float r1 = drand(rng);
   float r2 = drand(rng);
   float phi = 2 * kPi * r1;
   float z = rsqrt_exact(1 - r2);
+#if SRR_SINCOS && !defined(SRR_LIBM_DOUBLE)
+  float sp, cp;
+  gm::sincosf_(phi, sp, cp);  // = sinf_(phi), cosf_(phi)
+  float x = cp * 2 * rsqrt_exact(r2);
+  float y = sp * 2 * rsqrt_exact(r2);
+#else
   float x = rcos(phi) * 2 * rsqrt_exact(r2);  // cosf / sinf (glibc_mathf.h)
   float y = rsin(phi) * 2 * rsqrt_exact(r2);
+#endif
   return v3(x, y, z);
 }
 
