@@ -1877,7 +1877,7 @@ SRR_D V3 beckmann_sample_wh(const Beck& d, V3 wo, float u1, float u2) {  // :12-
 }
 
 #ifndef SRR_SINCOS
-#define SRR_SINCOS 0  // A/B: random_cosine_direction's sine and cosine from one sincosf_
+#define SRR_SINCOS 1  // random_cosine_direction's sine and cosine from one sincosf_ (A/B: -DSRR_SINCOS=0)
 #endif
 // pdf.h:10-18
 SRR_D V3 random_cosine_direction(Rng& rng) {
