@@ -29,6 +29,7 @@ struct SceneView {  // device pointers into the flattened tables (device_scene.h
   int quad_max;         // ...when at most this many lanes of the wave enter the mesh (else per lane)
   int mesh_obj;         // the world list's one top-level mesh object (k_paths CMP variant), else -1
   const float4* tri_pos;  // 4 float4 per triangle: p0, p1, p2, pad
+  const float4* tri_edge;  // 8 float4 per triangle i: p0, e1, e2 of i and i+1 packed (renderer.cpp)
   const TriShade* tri_shade;
   const DMedium* media;
   const DObvh* obvhs;                 // object BVHs (global memory)

@@ -112,6 +112,28 @@ SRR_D bool tri_hit(V3 p0, V3 p1, V3 p2, bool front, V3 o, V3 dir, float& t, floa
   return true;
 }
 
+// tri_hit's front test from p0 and the edges e1 = p1 - p0, e2 = p2 - p0 (the same
+// arithmetic after those two differences)
+SRR_D bool tri_hit_e(V3 p0, V3 e1, V3 e2, V3 o, V3 dir, float& t) {
+  V3 P = cross(dir, e2);
+  float det = dot(e1, P);
+  V3 T;
+  if (det > 0) T = o - p0;
+  else { T = p0 - o; det = -det; }
+  if (det < kUp1em4) return false;
+  float uu = dot(T, P);
+  if (uu < 0.0f || uu > det) return false;
+  V3 Q = cross(T, e1);
+  float vv = dot(dir, Q);
+  if (vv < 0.0f || vv + uu > det) return false;
+  float tt = dot(e2, Q);
+  float inv = 1.0f / det;
+  tt *= inv;
+  if (tt < kUp1em4) return false;
+  t = tt;
+  return true;
+}
+
 // Triangles are padded to 64 B (kTriStride float4) so a test touches one cache line.
 constexpr int kTriStride = 4;
 
@@ -430,6 +452,9 @@ constexpr bool LEAFQ = SRR_LEAFQ != 0;  // mesh_hit4's leaf-triangle queue (A/B:
 #ifndef SRR_TOPREG
 #define SRR_TOPREG 1  // the stack's top entry kept in registers (A/B: -DSRR_TOPREG=0)
 #endif
+#ifndef SRR_EDGEREC
+#define SRR_EDGEREC 1  // leaf pairs from packed p0 / e1 / e2 records (A/B: -DSRR_EDGEREC=0)
+#endif
 #ifndef SRR_LEAFPAIR
 #define SRR_LEAFPAIR 1  // one leaf (both triangles) per pass of the leaf queue (A/B: -DSRR_LEAFPAIR=0)
 #endif
@@ -572,6 +597,33 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
         if (TIMING) ++npass;
         const int t0 = q0 >> 1;
         const bool two = (q0 & 1) != 0;
+#if SRR_EDGEREC
+        if (!is_medium) {  // the packed edge record of t0: p0, e1, e2 of t0 and t0 + 1
+          const float4* lp = S.tri_edge + 8 * (size_t)t0;
+          const float4 w0 = lp[0], w1 = lp[1], w2 = lp[2], w3 = lp[3];
+          const float2 w4 = *(const float2*)(lp + 4);
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            if (j == 1 && !two) break;
+            const V3 p0 = j ? v3(w2.y, w2.z, w2.w) : v3(w0.x, w0.y, w0.z);
+            const V3 e1 = j ? v3(w3.x, w3.y, w3.z) : v3(w0.w, w1.x, w1.y);
+            const V3 e2 = j ? v3(w3.w, w4.x, w4.y) : v3(w1.z, w1.w, w2.x);
+            const int ti = t0 + j;
+            float t;
+            if (tri_hit_e(p0, e1, e2, r.o, dir, t) && (!found || wins(t, ti, best_t, best_i))) {
+              found = true;
+              best_t = t;
+              best_i = ti;
+            }
+          }
+          if (PRUNE && found && best_t * to_param < bound) bound = best_t * to_param;
+          q0 = q1;
+          q1 = q2;
+          q2 = q3;
+          q3 = -1;
+          continue;
+        }
+#endif
         const float4* tp = S.tri_pos + kTriStride * (size_t)t0;
         const float4* tq = tp + (two ? kTriStride : 0);
         const float4 a0 = tp[0], b0 = tp[1], c0 = tp[2];

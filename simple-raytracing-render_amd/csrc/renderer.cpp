@@ -67,6 +67,25 @@ int renderer_create_flat(const Flat& F, int device, srr_renderer** out, std::str
   float* n4q;
   RCHK(upload(&n4q, F.node4q, K));
   RCHK(upload(&tp, F.tri_pos, K));
+  // the walk's leaf-pair records (kernels.h SceneView::tri_edge): record i (128 B) holds
+  // p0, e1 = p1 - p0, e2 = p2 - p0 of triangles i and i+1 (the last repeats itself), the
+  // float differences tri_hit's front test forms -- computed here, they round the same
+  float* tedge;
+  {
+    const size_t nt = F.tri_pos.size() / 16;
+    std::vector<float> pr(32 * nt, 0.f);
+    for (size_t i = 0; i < nt; ++i)
+      for (int j = 0; j < 2; ++j) {
+        const float* q = &F.tri_pos[16 * std::min(i + j, nt - 1)];
+        float* o = &pr[32 * i + 9 * j];
+        for (int c = 0; c < 3; ++c) {
+          o[c] = q[c];
+          o[3 + c] = q[4 + c] - q[c];
+          o[6 + c] = q[8 + c] - q[c];
+        }
+      }
+    RCHK(upload(&tedge, pr, K));
+  }
   RCHK(upload(&ts, F.tri_shade, K));
   RCHK(upload(&md, F.media, K));
   RCHK(upload(&ob, F.obvhs, K));
@@ -144,6 +163,7 @@ int renderer_create_flat(const Flat& F, int device, srr_renderer** out, std::str
     if (n_mesh != 1) V.mesh_obj = -1;
   }
   V.tri_pos = (const float4*)tp;
+  V.tri_edge = (const float4*)tedge;
   V.tri_shade = ts;
   V.media = md;
   V.obvhs = ob;
