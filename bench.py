@@ -202,6 +202,15 @@ def cpu_baseline_reference(text, nx, ny, spp, max_depth, budget_s):
                       f"one single-threaded process per host CPU available to the job"}
 
 
+def _lib_sha256(path):
+    """first 16 hex digits of the library's SHA-256 (tools/counters.py records the same)"""
+    import hashlib
+    try:
+        return hashlib.sha256(open(path, "rb").read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
 def bench_line(a, text, cfg, nx, ny, spp, rays_total, elapsed, trace_ms, launches, world, workload_tail,
                parallelism, extra, rays_local=None, frame_spp=None, visits=None):
     """The JSON line (rank 0): value = every device's world rays over the slowest
@@ -225,19 +234,8 @@ def bench_line(a, text, cfg, nx, ny, spp, rays_total, elapsed, trace_ms, launche
     wave = bool(os.environ.get("SRR_ENGINE") == "wave")
     kernel_name = ("k_trace (wavefront engine)" if wave else
                    "k_paths (path-resident persistent kernel: trace + shade)")
+    # measured HBM bytes: the counter summary of this build (below), else null
     traffic = None
-    # measured HBM bytes of k_paths (tools/pmc_traffic.py).  A summary that records its
-    # frame's world rays is priced per world ray on this run's launches; an older one only
-    # stands for the default single-GPU frame it was measured on
-    pmc = os.path.join(ROOT, "profiles", f"pmc_{a.scene}{key[len(CONFIG_KEY[a.scene]):]}.json")
-    default_frame = (world == 1 and a.plan == "tiles" and (nx, ny, spp) == (cfg["nx"], cfg["ny"], cfg["spp"]))
-    if os.path.exists(pmc) and launches:
-        pj = json.load(open(pmc))
-        if pj.get("kernel", "") in kernel_name:
-            if pj.get("world_rays_per_launch"):
-                traffic = round(pj["hbm_bytes_per_launch"] / pj["world_rays_per_launch"] * rays / launches)
-            elif default_frame:
-                traffic = pj.get("hbm_bytes_per_launch")
     out = {
         "metric": "Msamples/s (rays x bounces) + HBM GB/s vs roofline, Cornell+teapot 1024spp",
         "value": round(value, 3),
@@ -287,7 +285,30 @@ def bench_line(a, text, cfg, nx, ny, spp, rays_total, elapsed, trace_ms, launche
             if j.get("world_rays_per_launch"):
                 cj, cnt = j, f
                 break
-    cnt_round = os.path.basename(os.path.dirname(cnt)) if cnt else ""
+    # a counter summary prices this run only when it profiled the library running here
+    # (tools/counters.py records its SHA-256): instruction counts of another build are not
+    # this kernel's
+    from srr import capi
+    sha = _lib_sha256(capi.LIB_PATH)
+    out["roofline"]["build"] = {"lib": os.path.relpath(capi.LIB_PATH, ROOT), "lib_sha256": sha}
+    if cj is not None and (cj.get("build") or {}).get("lib_sha256") != sha:
+        out["roofline"]["issue"] = None
+        out["roofline"]["issue_note"] = (
+            f"{os.path.relpath(cnt, ROOT)} profiled library "
+            f"{(cj.get('build') or {}).get('lib_sha256') or 'unrecorded'}, this run's is {sha}: its counters are "
+            f"not this build's, so no issue roofline is derived from them")
+        cj = None
+    # a scene whose sphere runs go through sgroup_hit's BVH (ball_scenes, random_scene) does not
+    # perform the reference's linear list of sphere tests that its B_cfg prices
+    # (hitable_list.h:21-33): those bytes are not this kernel's traversal
+    if a.scene in ("ball", "random") and not os.environ.get("SRR_SGROUP", "1") == "0":
+        for k in ("achieved", "frac"):
+            out["roofline"][k] = None
+        out["roofline"]["frac_note"] = (
+            f"B_cfg {b_cfg:.0f} B counts the reference's linear list ({counts_json[key].get('N_prim', '?')} "
+            f"primitive tests per world ray); srr answers the list's sphere runs through a BVH (sgroup_hit) "
+            f"with the same result, so the reference's algorithmic bytes would overstate this kernel's "
+            f"traffic (frac > 1): not reported")
     if cj is not None and trace_ms > 0 and rays > 0:
         insts_per_ray = cj["raw_per_launch"]["SQ_INSTS_VALU"] / cj["world_rays_per_launch"]
         clock = cj.get("clock_ghz") or 2.4
@@ -305,7 +326,7 @@ def bench_line(a, text, cfg, nx, ny, spp, rays_total, elapsed, trace_ms, launche
         hbm = cj.get("hbm") or {}
         # the counter summary's HBM bytes (FETCH_SIZE / WRITE_SIZE passes of the same
         # profiling run) take precedence over an older separate traffic summary
-        if hbm.get("total_bytes") and (traffic is None or cnt_round >= "r04"):
+        if hbm.get("total_bytes"):
             # measured HBM bytes per world ray of the profiled frame, priced on this run's launches
             traffic = round(hbm["total_bytes"] / cj["world_rays_per_launch"] * rays / max(launches, 1))
             out["roofline"]["traffic"] = traffic

@@ -184,6 +184,8 @@ typedef struct srr_stats {
                            /* its LDS part into the global extension           */
   int64_t mixture_capped;  /* path engine: resampling loops (Raytracing_n.cpp:79-83) */
                            /* stopped by the 100,000-attempt cap   */
+  int64_t walks_suspended; /* path engine: mesh walks continued in a later wave-  */
+                           /* iteration (SRR_WALK_Q)              */
 } srr_stats;
 
 /* Flatten the scene and upload it to HIP device `device`. */
@@ -199,7 +201,10 @@ void srr_renderer_destroy(srr_renderer* r);
  * once, then ONE frame-end gather of the packed shard slabs to device_ids[0] over
  * RCCL (ncclCommInitAll communicator, ncclSend / ncclRecv in one group) and a
  * scatter into the image there: d_mean is a device_ids[0] pointer of nx*ny*3
- * floats, bitwise the one-device frame.  The calls return after the gather.
+ * floats, bitwise the one-device frame.  srr_render / srr_render_device return
+ * after the gather; srr_render_device_async enqueues the gather on the GPU behind
+ * the shards' frames (and behind the caller's legacy-stream work on device_ids[0])
+ * and returns at once -- the host waits only in srr_render_wait.
  * device_ids may repeat a device (a rehearsal on one GPU): the gather is then
  * device copies, as with SRR_MULTI_TRANSPORT=copy.  No KEEP_PATHS / CONTINUE
  * (SRR_EINVAL); srr_accum_* and srr_copy_paths are single-device. */
@@ -236,7 +241,10 @@ int srr_render_device(srr_renderer* r, const srr_params* p, float* d_mean, srr_s
  * bounce records (16 B x max_depth per persistent lane) and sums; the
  * synchronous slot keeps its own window too, so alternating the two modes
  * reallocates nothing (the other mode's windows are given back only when an
- * allocation would run the device out of memory). */
+ * allocation would run the device out of memory).  Per renderer the windows are
+ * thus at most 3 x SRR_WINDOW_MB; the peers of a multi-device renderer that share
+ * a device (device_ids repeating it) split SRR_WINDOW_MB between them, so a
+ * device holds at most 3 x SRR_WINDOW_MB of windows either way. */
 int srr_render_device_async(srr_renderer* r, const srr_params* p, float* d_mean, int64_t* ticket);
 /* Wait for an async frame and return its stats (each ticket once). */
 int srr_render_wait(srr_renderer* r, int64_t ticket, srr_stats* stats);

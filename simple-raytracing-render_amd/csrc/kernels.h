@@ -127,6 +127,11 @@ struct PathWork {
   int deep_tries;         // coop_mixture: failed attempts after which a path takes every free lane (32)
   float* slow_rays;       // diagnostics build (-DSRR_SLOW_RAYS=ticks): [65536][16] records of slow world hits
   unsigned* slow_count;
+  // suspendable mesh walks (kernels.hip TraceCtx::walk_thr): a lane's walk, after a node
+  // step, stops for this wave-iteration once at most walk_q / 64 of the wave's lanes in a
+  // path are still walking (0: never); its state goes to the [3][lanes] float4 save area
+  // that follows gstack's gstack_cap x lanes entries (so walks suspend only with gstack)
+  int walk_q;
 };
 #ifndef SRR_KSTACK
 #define SRR_KSTACK 8
@@ -142,7 +147,8 @@ constexpr int kPathsLdsNodes = SRR_LDS_NODES;  // BVH4 nodes cached in LDS by k_
 void dump_trace_timing();
 int paths_lanes_per_device(const SceneView& S, int device);  // persistent grid capacity
 int paths_block_lanes(const SceneView& S);  // k_paths lanes per block for this scene (256 or 1,024)
-void launch_paths(const SceneView& S, const PathWork& W, int all_families, hipStream_t st);
+// 0, or -1 (nothing launched) when W.stack_cap exceeds the kernels' LDS stack (kStack)
+int launch_paths(const SceneView& S, const PathWork& W, int all_families, hipStream_t st);
 // device known-answer tests (srr_device_kat); kind = dev::KatKind
 // device tables of the camera / light KATs (srr_device_kat builds them with the
 // host scene code: one camera per record, one light list for all records)

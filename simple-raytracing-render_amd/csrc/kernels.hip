@@ -298,6 +298,17 @@ struct TraceCtx {
   int gst_cap = 0;
   int gst_stride = 0;
   int slot = 0;
+  // Suspendable mesh walks (k_paths, TR_SUSP): a lane whose walk has
+  // taken a node step in this call leaves it once at most walk_thr lanes of its
+  // wave are still walking (<= 0: never), its walk state saved in the save area that
+  // follows the stack's global extension (walk_save(): [3][gst_stride] float4 at
+  // `slot`); `resume` (in) continues the walk saved there, `susp` (out) says the
+  // lane suspended.  All three are per-lane VGPR ints (vreg()): the path kernel's
+  // scalar registers are full, and every scalar value live across the walk loop
+  // spills to VGPR lanes (v_writelane / v_readlane in the loop)
+  int walk_thr = -1;
+  mutable int resume = 0;
+  mutable int susp = 0;
   // SRR_TIMING diagnostics (wave-uniform): cycles inside mesh traversals, steps
   mutable uint64_t mesh_cycles = 0;
   mutable int mesh_steps = 0;       // node steps of the wave's longest walk
@@ -324,6 +335,17 @@ struct TraceCtx {
 // tmin-clipped entry, as round 1 did, lost the nearer self-hits of rays leaving
 // the mesh's own surface: 1,115 world rays of the 512x512x1024 C2 frame.)
 constexpr float kPruneSlack = 1.0625f;
+
+// a value the compiler must keep in a VGPR (see TraceCtx::walk_thr)
+SRR_D int vreg(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+// the suspended-walk save area: [3][gst_stride] float4 right after the stack's
+// global extension (renderer.cpp allocates both at once), lane `slot`, word w
+SRR_D float4* walk_save(const TraceCtx& cx, int w) {
+  return (float4*)(cx.gst + (size_t)cx.gst_cap * cx.gst_stride) + ((size_t)w * cx.gst_stride + cx.slot);
+}
 
 // A NaN t bound (tmax): the world list's closest-so-far goes NaN when an
 // earlier object reports a hit at t = NaN -- e.g. a ray lying in an xz_rect
@@ -459,9 +481,14 @@ constexpr bool LEAFQ = SRR_LEAFQ != 0;  // mesh_hit4's leaf-triangle queue (A/B:
 #define SRR_LEAFPAIR 1  // one leaf (both triangles) per pass of the leaf queue (A/B: -DSRR_LEAFPAIR=0)
 #endif
 
-template <bool PRUNE, bool TIMING = false, bool Q = false, int STRIDE = kTraceBlock>
+// SUSP: the walk may stop part-way (TraceCtx::walk_thr) and continue in a later
+// call with TraceCtx::resume; its state at the loop top -- next node, stack depth
+// and top entry (the deeper entries stay in the lane's LDS stack and global
+// extension, which nothing else touches), best hit, bound, flags -- is all it needs.
+template <bool PRUNE, bool TIMING = false, bool Q = false, int STRIDE = kTraceBlock, bool SUSP = false>
 SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmin, float tmax, bool is_medium,
                      MeshHit& out, const TraceCtx& cx) {
+  static_assert(!SUSP || (SRR_TOPREG && !Q), "suspendable walks: the register top entry, 128-B nodes");
   if (const uint64_t nanm = __ballot(!(tmax == tmax))) {  // NaN bound: the fold over all triangles
     bool f = false;
     float bt = 0;
@@ -496,6 +523,23 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
   int top_n = -1;
   float top_t = 0.f;
 #endif
+  if constexpr (SUSP) {
+    if (cx.resume) {  // the walk this lane suspended in an earlier wave-iteration
+      const float4 a = *walk_save(cx, 0), b = *walk_save(cx, 1);
+      node = __float_as_int(a.x);
+      sp = __float_as_int(a.y);
+      top_n = __float_as_int(a.z);
+      top_t = a.w;
+      best_t = b.x;
+      best_i = __float_as_int(b.y);
+      found = best_i >= 0;
+      bound = b.z;
+      const int fl = __float_as_int(b.w);
+      overflow = (fl & 1) != 0;
+      deep = (fl & 2) != 0;
+      cx.resume = 0;
+    }
+  }
   for (;;) {
     if (TIMING) {
       asm volatile("" ::"v"(node), "v"(sp));
@@ -768,8 +812,9 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
     // the stack's top entry is also kept in registers (top_n, top_t: entry sp - 1
     // whenever sp > 0), so a pop has its node at once and reads the entry below it
     // from LDS while the next step runs
+    int nx = -1;  // the next node (the nearest child, or the nearest pending subtree), -1: done
     if (kn[0] >= 0) {
-      node = kn[0];
+      nx = kn[0];
 #pragma unroll
       for (int c = 3; c >= 1; --c) {
         if (kn[c] < 0) continue;
@@ -789,24 +834,34 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
           overflow = true;
         }
       }
-      continue;
-    }
-    int nx = -1;
-    while (sp > 0) {
-      --sp;
-      const int cand = top_n;
-      const float ct = top_t;
-      if (sp > 0) {  // the new top
-        if (sp - 1 < cx.st_cap) {
-          top_n = cx.st_node[(sp - 1) * STRIDE];
-          top_t = cx.st_t[(sp - 1) * STRIDE];
-        } else {
-          const int2 e = cx.gst[(size_t)(sp - 1 - cx.st_cap) * cx.gst_stride + cx.slot];
-          top_n = e.x;
-          top_t = __int_as_float(e.y);
+    } else {
+      while (sp > 0) {
+        --sp;
+        const int cand = top_n;
+        const float ct = top_t;
+        if (sp > 0) {  // the new top
+          if (sp - 1 < cx.st_cap) {
+            top_n = cx.st_node[(sp - 1) * STRIDE];
+            top_t = cx.st_t[(sp - 1) * STRIDE];
+          } else {
+            const int2 e = cx.gst[(size_t)(sp - 1 - cx.st_cap) * cx.gst_stride + cx.slot];
+            top_n = e.x;
+            top_t = __int_as_float(e.y);
+          }
         }
+        if (!(PRUNE && ct > bound)) { nx = cand; break; }
       }
-      if (!(PRUNE && ct > bound)) { nx = cand; break; }
+    }
+    if constexpr (SUSP) {
+      // (SUSP) the walk also stops, to continue in a later wave-iteration, once at most
+      // walk_thr of the wave's lanes have a next node (wave-uniform; every lane has taken
+      // this step, so each progresses): one exit with the finished walks, node = next
+      if (nx < 0 || (int)__popcll(__ballot(nx >= 0)) <= cx.walk_thr) {
+        node = nx;
+        break;
+      }
+      node = nx;
+      continue;
     }
 #else
     if (kn[0] >= 0) {
@@ -848,6 +903,16 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
     if (nx < 0) break;
     node = nx;
   }
+  bool suspended = false;
+  if constexpr (SUSP) {
+    if (node >= 0) {  // stopped with a next node: the walk's state at the top of that step
+      *walk_save(cx, 0) = make_float4(__int_as_float(node), __int_as_float(sp), __int_as_float(top_n), top_t);
+      *walk_save(cx, 1) =
+          make_float4(best_t, __int_as_float(best_i), bound, __int_as_float((overflow ? 1 : 0) | (deep ? 2 : 0)));
+      cx.susp = 1;
+      suspended = true;
+    }
+  }
   if (cx.ctr && !TIMING) {
     atomicAdd(cx.ctr, (unsigned long long)nbox);
     atomicAdd(cx.ctr + 1, (unsigned long long)ntri);
@@ -882,13 +947,14 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
     cx.mesh_walkers += walk;
     cx.mesh_cycles += __builtin_amdgcn_s_memtime() - tm_enter;
   }
-  if (cx.ovf && cx.gst) {  // traversals that used the global stack (one atomic per wave)
-    const uint64_t dm = __ballot(deep);
+  if (cx.ovf && cx.gst) {  // traversals that used the global stack (one atomic per wave; a suspended walk counts when it ends)
+    const uint64_t dm = __ballot(deep && !suspended);
     if (dm && (int)__lane_id() == __ffsll((unsigned long long)dm) - 1) atomicAdd(cx.ovf + 1, (unsigned long long)__popcll(dm));
   }
 #ifdef SRR_SLOW_RAYS
   cx.last_steps += (int)(nbox / 4) | (overflow ? 1 << 30 : 0) | (deep ? 1 << 29 : 0);
 #endif
+  if (SUSP && suspended) return false;  // (the caller sees cx.susp)
   if (overflow) {  // rare: exact re-walk
     if (cx.ovf) atomicAdd(cx.ovf, 1ull);
     return mesh_hit<false>(S, m, r, tmin, tmax, is_medium, out, cx.ctr);
@@ -913,6 +979,10 @@ constexpr int TR_QUAD = 32;
 constexpr int TR_Q = 64;  // meshes traced over the compressed 64-B nodes (SceneView::node4q)
 constexpr int TR_BIG = 128;  // the 1,024-lane path kernel: LDS stacks with stride 1,024
 constexpr int tr_stride(int tr) { return (tr & TR_BIG) ? 1024 : kTraceBlock; }
+constexpr int TR_SUSP = 256;  // the path kernel: mesh walks may suspend and resume (TraceCtx::walk_thr)
+#ifndef SRR_SUSP
+#define SRR_SUSP 1  // (A/B: -DSRR_SUSP=0 builds k_paths without suspendable walks)
+#endif
 
 template <int CTRL>
 SRR_D int quad_dpp(int x) { return __builtin_amdgcn_update_dpp(x, x, CTRL, 0xF, 0xF, false); }
@@ -1391,7 +1461,7 @@ SRR_D bool basic_hit(const SceneView& S, const DObj& ob, const Ray& lr, float tm
       else if (TR & TR_Q)
         hit = mesh_hit4<tr_mode(TR) != TR_BVH4, false, true, tr_stride(TR)>(S, m, lr, tmin, tmax, is_medium, mh, cx);
       else
-        hit = mesh_hit4<tr_mode(TR) != TR_BVH4, tr_mode(TR) == TR_BVH4_TIMED, false, tr_stride(TR)>(
+        hit = mesh_hit4<tr_mode(TR) != TR_BVH4, tr_mode(TR) == TR_BVH4_TIMED, false, tr_stride(TR), (TR & TR_SUSP) != 0>(
             S, m, lr, tmin, tmax, is_medium, mh, cx);
       if (!hit) return false;
       h.t = mh.t;
@@ -1510,13 +1580,32 @@ SRR_D void world_objs(const SceneView& S, const Ray& r, Rng& rng, const TraceCtx
   }
 }
 
+// TR_SUSP: a lane's mesh walk may suspend (cx.susp): the lane leaves the list
+// there, its list state (object, closest-so-far, record so far) saved beside the
+// walk's; a resuming lane (cx.resume) restores it, passes over the objects before
+// its mesh (their tests are done) and continues the walk, then the list.  The
+// objects stay in list order for every lane, so the result is the same.
 template <bool MEDIA, int TR>
 SRR_D WorldHit world_hit(const SceneView& S, const Ray& r, Rng& rng, const TraceCtx& cx) {
   WorldHit w{-1, -1, 0};
   float closest = FLT_MAX;  // numeric_limits<float>::max(), Raytracing_n.cpp:58
   const float tmin = 0.001f;
+  constexpr bool SUSP = (TR & TR_SUSP) != 0;
+  int k_res = -1;  // (SUSP) the object whose walk this lane resumes
+  if constexpr (SUSP) {
+    if (cx.resume) {
+      const float4 v = *walk_save(cx, 2);
+      k_res = __float_as_int(v.x);
+      closest = v.y;
+      w.obj = __float_as_int(v.z);
+      w.prim = __float_as_int(v.w);
+      w.t = closest;
+    }
+  }
   for (int k = 0; k < S.n_world; ++k) {
     const DObj ob = maybe_uni<SRR_UNIFORM != 0>(wload<TR>(S.objs, k));
+    // (a per-lane skip, not a break: the object loop stays wave-uniform)
+    if (SUSP && (cx.susp || k < k_res)) continue;
     Ray lr = chain_in<TR, SRR_UNIFORM != 0>(S, ob, r);
     ObjHit h;
     bool hit;
@@ -1525,6 +1614,10 @@ SRR_D WorldHit world_hit(const SceneView& S, const Ray& r, Rng& rng, const Trace
       h.prim = -1;
     } else {
       hit = basic_hit<TR, SRR_UNIFORM != 0>(S, ob, lr, tmin, closest, false, h, cx);
+    }
+    if (SUSP && cx.susp) {
+      *walk_save(cx, 2) = make_float4(__int_as_float(k), closest, __int_as_float(w.obj), __int_as_float(w.prim));
+      continue;
     }
     if (hit) {
       closest = h.t;
@@ -3039,7 +3132,7 @@ __global__ void __launch_bounds__(BS, MINB) SRR_PATHS_VGPR_ATTR k_paths(PathsArg
   (void)A;  // read through paths_args()
   // TIMED (diagnostics): per-wave cycles in refill / world hit (mesh part) / record+scatter / fold
   uint64_t tp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  // TIMED family diagnostics -> W.counters[16..27]: ticks in the BECK / SPEC / DIFF-set-up
+  // TIMED family diagnostics -> W.counters[16..35]: ticks in the BECK / SPEC / DIFF-set-up
   // branches of the per-lane scatter, iterations each branch ran, lanes it ran for;
   // lanes in a path; the longest walk's node steps, all lanes' steps, walking lanes (wave time
   // in the mesh is tp[2])
@@ -3048,7 +3141,9 @@ __global__ void __launch_bounds__(BS, MINB) SRR_PATHS_VGPR_ATTR k_paths(PathsArg
   // WL: world tables staged in LDS (they fit in kWorldLdsBytes); otherwise read
   // from global memory (large object lists, e.g. random_scene's ~490 spheres)
   // QUAD: meshes traced by mesh_hit4_quad (large BVHs, SceneView::quad_trace)
-  constexpr int TR = TR_BVH4_PRUNE | (WL ? TR_WL : 0) | (QUAD ? TR_QUAD : 0) | (CQ ? TR_Q : 0) | (BS == 1024 ? TR_BIG : 0);
+  // (per-lane walks over 128-B nodes may suspend: TR_SUSP, PathWork::walk_q)
+  constexpr int TR = TR_BVH4_PRUNE | (WL ? TR_WL : 0) | (QUAD ? TR_QUAD : 0) | (CQ ? TR_Q : 0) | (BS == 1024 ? TR_BIG : 0) |
+                     ((QUAD || CQ || !SRR_SUSP) ? 0 : TR_SUSP);
   __shared__ uint4 s_world[WL ? kWorldLdsBytes / 16 : 1];
   // the scene as a phase reads it: scalar loads of the fields it uses, the world
   // tables re-pointed into LDS (WL)
@@ -3116,8 +3211,13 @@ __global__ void __launch_bounds__(BS, MINB) SRR_PATHS_VGPR_ATTR k_paths(PathsArg
   Ray r{};
   Rng rng{};
   int depth = 0;
+  int walking = 0;  // (TR_SUSP) this lane's world hit is a suspended mesh walk
   uint32_t nrays = 0;
-  uint32_t n_capped = 0;  // resampling loops stopped by kMixtureGuard
+  // this lane's events, two counts in one register (each loop-carried VGPR is dear in the
+  // ALLFAM variants): resampling loops stopped by kMixtureGuard in bits 0-11 (each costs
+  // 100,000 attempts: a lane never reaches 4,096) and suspended mesh walks from bit 12
+  uint32_t n_events = 0;
+  constexpr uint32_t kCapped = 1, kSuspended = 1u << 12;
   uint32_t n_iter = 0, max_rounds = 0;  // wave-iterations, most mixture rounds (SRR_WAVE_TIMES diagnostics)
   for (;;) {
     ++n_iter;
@@ -3223,6 +3323,7 @@ __global__ void __launch_bounds__(BS, MINB) SRR_PATHS_VGPR_ATTR k_paths(PathsArg
     // the whole wave (coop_mixture), then its record is written
     bool diff = false, pend = false;
     int natt = 0;  // (TIMED: mixture attempts of this lane's Beckmann scatter)
+    uint64_t fam_dt[3] = {0, 0, 0};  // (TIMED: this lane's ticks in the BECK / SPEC / DIFF-set-up branch)
     DiffSetup ds{};
     V3 d_atten = v3(0.f), d_n = v3(0.f), d_dir = v3(0.f);
     float d_pdf = 0;
@@ -3243,12 +3344,27 @@ __global__ void __launch_bounds__(BS, MINB) SRR_PATHS_VGPR_ATTR k_paths(PathsArg
       cx.gst_cap = W.gstack ? W.gstack_cap : 0;
       cx.gst_stride = W.lanes;
       cx.slot = slot;
+      if constexpr ((TR & TR_SUSP) != 0) {
+        // suspend walks once at most walk_q / 64 of the wave's lanes in a path still walk
+        // (the save area follows the global stack extension: none without it)
+        // (walk_q 0: threshold 0, and a walk only stops when its lanes all finished)
+        cx.walk_thr = vreg((int)((__popcll(__ballot(true)) * (uint32_t)paths_args()->W.walk_q) >> 6));
+        cx.resume = walking;
+        cx.susp = vreg(0);
+      }
 #ifdef SRR_SLOW_RAYS
       const uint64_t t_w0 = __builtin_amdgcn_s_memrealtime();
       cx.last_steps = 0;
       const Ray r_in = r;
 #endif
-      w = world_hit<MEDIA, TIMED ? (TR_BVH4_TIMED | (WL ? TR_WL : 0)) : TR>(S, r, rng, cx);
+      w = world_hit<MEDIA, TIMED ? (TR_BVH4_TIMED | (WL ? TR_WL : 0) | TR_SUSP) : TR>(S, r, rng, cx);
+      if constexpr ((TR & TR_SUSP) != 0) {
+        walking = cx.susp;  // (its record, scatter and fold wait for the walk's end)
+        if (walking) {
+          w.obj = -1;
+          n_events += kSuspended;
+        }
+      }
 #ifdef SRR_SLOW_RAYS
       // diagnostics build: every lane of a world hit slower than SRR_SLOW_RAYS
       // ticks (100 MHz) records its ray: g, depth, o, d, time, ticks, steps, hit
@@ -3286,7 +3402,7 @@ __global__ void __launch_bounds__(BS, MINB) SRR_PATHS_VGPR_ATTR k_paths(PathsArg
         tf[17] += cx.step_parts[2];
         tq = t;
       }
-      done = true;
+      done = !walking;
     }
     if (nxt_armed && !nxt_ready) {  // (uniform: every lane of the wave is here)
       nxt_base = __builtin_amdgcn_readfirstlane(nxt_lane0);
@@ -3330,7 +3446,7 @@ __global__ void __launch_bounds__(BS, MINB) SRR_PATHS_VGPR_ATTR k_paths(PathsArg
           d_n = h.n;
           diff = pend = true;
           done = false;
-          if (TIMED) tf[2] += __builtin_amdgcn_s_memtime() - tq;
+          if (TIMED) fam_dt[2] = __builtin_amdgcn_s_memtime() - tq;
         } else {
           const DMat M = S.mats[h.mat];
           float4 rec;
@@ -3341,14 +3457,14 @@ __global__ void __launch_bounds__(BS, MINB) SRR_PATHS_VGPR_ATTR k_paths(PathsArg
           if (!ALLFAM || fam == FAM_DIFF) scatter<FAM_DIFF>(S, M, r.d, r.tm, h.p, h.n, h.u, h.v, rng, rec, sp, nd, nt);
           else if (fam == FAM_BECK) {
             scatter<FAM_BECK>(S, M, r.d, r.tm, h.p, h.n, h.u, h.v, rng, rec, sp, nd, nt, TIMED ? &natt : nullptr);
-            if (TIMED) tf[0] += __builtin_amdgcn_s_memtime() - tb;
+            if (TIMED) fam_dt[0] = __builtin_amdgcn_s_memtime() - tb;
           } else {
             scatter<FAM_SPEC>(S, M, r.d, r.tm, h.p, h.n, h.u, h.v, rng, rec, sp, nd, nt);
-            if (TIMED) tf[1] += __builtin_amdgcn_s_memtime() - tb;
+            if (TIMED) fam_dt[1] = __builtin_amdgcn_s_memtime() - tb;
           }
           if (depth >= W.max_depth || slot >= W.lanes) atomicOr(W.err, 2);
           else rec_store(rec_at(W, depth), rec);
-          if (!sp && S.n_lights > 0 && rec.w == 0) ++n_capped;  // the loop reached kMixtureGuard
+          if (!sp && S.n_lights > 0 && rec.w == 0) n_events += kCapped;  // the loop reached kMixtureGuard
           r = Ray{h.p, nd, nt};
           ++depth;
           done = false;
@@ -3363,6 +3479,13 @@ __global__ void __launch_bounds__(BS, MINB) SRR_PATHS_VGPR_ATTR k_paths(PathsArg
       }
       tf[18] += sum;
       tf[19] += mx;
+      // the family branches' wave time this iteration: the longest of their lanes' stamps
+      // (lanes of one branch run it together; lanes outside it stamped 0)
+      for (int q = 0; q < 3; ++q) {
+        uint64_t m = fam_dt[q];
+        for (int o = 32; o > 0; o >>= 1) m = max(m, (uint64_t)__shfl_xor((unsigned long long)m, o));
+        tf[q] += m;
+      }
     }
     if (__ballot(pend)) {
       const SceneView S = view();
@@ -3384,7 +3507,7 @@ __global__ void __launch_bounds__(BS, MINB) SRR_PATHS_VGPR_ATTR k_paths(PathsArg
     }
     if (diff) {  // the rest of scatter<FAM_DIFF>: scattering_pdf and the record
       const PathWork W = work();
-      if (d_pdf == 0) ++n_capped;  // the loop reached kMixtureGuard
+      if (d_pdf == 0) n_events += kCapped;  // the loop reached kMixtureGuard
       float c = dot(d_n, unit_vector(d_dir));  // material.h:100-105, 134-138
       if (c < 0) c = 0;
       const V3 as = d_atten * (c / kPi);
@@ -3459,13 +3582,20 @@ __global__ void __launch_bounds__(BS, MINB) SRR_PATHS_VGPR_ATTR k_paths(PathsArg
     atomicAdd(W.counters + 14, (unsigned long long)tp[7]);
     for (int q = 0; q < 20; ++q) atomicAdd(W.counters + 16 + q, (unsigned long long)tf[q]);
   }
+
   unsigned long long tot = nrays;
   for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
   if (lane_id() == 0 && tot) atomicAdd(W.counters, tot);
-  if (__ballot(n_capped != 0)) {
-    unsigned long long cap = n_capped;
-    for (int o = 32; o > 0; o >>= 1) cap += __shfl_xor(cap, o);
-    if (lane_id() == 0) atomicAdd(W.counters + 15, cap);
+  if (__ballot(n_events != 0)) {
+    unsigned long long cap = n_events & (kSuspended - 1), su = n_events / kSuspended;
+    for (int o = 32; o > 0; o >>= 1) {
+      cap += __shfl_xor(cap, o);
+      su += __shfl_xor(su, o);
+    }
+    if (lane_id() == 0) {
+      if (cap) atomicAdd(W.counters + 15, cap);
+      if (su) atomicAdd(W.counters + 36, su);
+    }
   }
   if (W.wave_times && lane_id() == 0) {  // diagnostics: start, exit, world rays, wave-iterations
     const size_t wv = (size_t)(blockIdx.x * blockDim.x + threadIdx.x) / 64;
@@ -4060,7 +4190,10 @@ int paths_lanes_per_device(const SceneView& S, int device) {
   return cus * per_cu * dev::kPathsBlock;
 }
 
-void launch_paths(const SceneView& S, const PathWork& W, int all_families, hipStream_t st) {
+int launch_paths(const SceneView& S, const PathWork& W, int all_families, hipStream_t st) {
+  // the kernels index kStack LDS entries per lane: a host built with a larger
+  // SRR_KSTACK is refused here (round 4 ran such a mix once: an illegal address)
+  if (W.stack_cap < 1 || W.stack_cap > dev::kStack) return -1;
   const dev::PathsArgs args{S, W};
   const int blocks = W.lanes / dev::kPathsBlock;
   static const bool force_global = getenv("SRR_WORLD_GLOBAL") != nullptr;  // A/B diagnostics
@@ -4076,7 +4209,7 @@ void launch_paths(const SceneView& S, const PathWork& W, int all_families, hipSt
       else SRR_LAUNCH_PATHS_G(false, false);
     }
 #undef SRR_LAUNCH_PATHS_G
-    return;
+    return 0;
   }
   const int bs = paths_block_lanes(S);
   const int blocks_b = W.lanes / bs;
@@ -4121,6 +4254,7 @@ void launch_paths(const SceneView& S, const PathWork& W, int all_families, hipSt
 #undef SRR_LAUNCH_PATHS_DIAG
 #undef SRR_LAUNCH_PATHS_B
 #undef SRR_LAUNCH_PATHS
+  return 0;
 }
 
 int launch_merl_lookup(const double* table, int64_t n, const double* angles, double* rgb, int32_t* cell) {

@@ -100,6 +100,8 @@ struct PendingFrame {
   std::vector<int64_t> tickets;  // each device's srr_render_device_async ticket
 };
 
+
+
 }  // namespace
 
 struct Multi {
@@ -108,7 +110,11 @@ struct Multi {
   bool use_rccl = false;
   std::vector<ncclComm_t> comms;
   std::vector<hipStream_t> xst;  // per-device exchange stream
-  hipEvent_t ev_x0 = nullptr, ev_x1 = nullptr;
+  // per buffer set (frames in flight each have their own): on devs[0] the exchange's
+  // start / end and the caller's legacy-stream work it follows; per device the end of
+  // its send (RCCL)
+  hipEvent_t ev_x0[2] = {nullptr, nullptr}, ev_x1[2] = {nullptr, nullptr}, ev_in[2] = {nullptr, nullptr};
+  std::vector<hipEvent_t> ev_sent[2];
   // the frame plan: {nx, ny, tile}; shard pixel lists and offsets in the packed frame
   int key[3] = {-1, -1, -1};
   std::vector<std::vector<int32_t>> shard_pix;
@@ -136,16 +142,19 @@ struct Multi {
         if (c) rccl().CommDestroy(c);
     for (size_t k = 0; k < devs.size(); ++k) {
       (void)hipSetDevice(devs[k]);
-      for (int b = 0; b < 2; ++b)
+      for (int b = 0; b < 2; ++b) {
         if (k < slab[b].size() && slab[b][k]) (void)hipFree(slab[b][k]);
+        if (k < ev_sent[b].size() && ev_sent[b][k]) (void)hipEventDestroy(ev_sent[b][k]);
+      }
       if (k < xst.size() && xst[k]) (void)hipStreamDestroy(xst[k]);
     }
     if (!devs.empty()) {
       (void)hipSetDevice(devs[0]);
       for (float* p : packed) (void)hipFree(p);
       (void)hipFree(d_index);
-      if (ev_x0) (void)hipEventDestroy(ev_x0);
-      if (ev_x1) (void)hipEventDestroy(ev_x1);
+      for (int b = 0; b < 2; ++b)
+        for (hipEvent_t e : {ev_x0[b], ev_x1[b], ev_in[b]})
+          if (e) (void)hipEventDestroy(e);
     }
     for (srr_renderer* r : peers) srr_renderer_destroy(r);
   }
@@ -235,9 +244,21 @@ int multi_create(const Scene& sc, int n, const int* ids, srr_renderer** out, std
     MCHK(hipSetDevice(ids[k]));
     MCHK(hipStreamCreateWithFlags(&M.xst[k], hipStreamNonBlocking));
   }
-  MCHK(hipSetDevice(ids[0]));
-  MCHK(hipEventCreate(&M.ev_x0));
-  MCHK(hipEventCreate(&M.ev_x1));
+  for (int b = 0; b < 2; ++b) {
+    M.ev_sent[b].assign(n, nullptr);
+    for (int k = 0; k < n; ++k) {
+      MCHK(hipSetDevice(ids[k]));
+      MCHK(hipEventCreateWithFlags(&M.ev_sent[b][k], hipEventDisableTiming));
+    }
+    MCHK(hipSetDevice(ids[0]));
+    MCHK(hipEventCreate(&M.ev_x0[b]));
+    MCHK(hipEventCreate(&M.ev_x1[b]));
+    MCHK(hipEventCreateWithFlags(&M.ev_in[b], hipEventDisableTiming));
+  }
+  // peers sharing a device (a one-GPU rehearsal) split the sample-window budget, so
+  // the device holds what one renderer would (renderer.cpp paths_enqueue)
+  for (int k = 0; k < n; ++k)
+    M.peers[k]->window_share = (int)std::count(ids, ids + n, ids[k]);
   if (M.use_rccl) {
     const Rccl& R = rccl();
     if (!R.so) {
@@ -297,14 +318,21 @@ int stage(Multi& M, const srr_params* p, int b, std::string& err) {
     const int64_t total = multi_plan(p, n, &M.shard_pix, index.data(), off.data(), err);
     if (total < 0) return (int)total;
     MCHK(hipSetDevice(M.devs[0]));
+    // the plan is invalid from here until its index is staged: a failure below leaves
+    // no key that a later frame could take for the staged one
+    M.key[0] = -1;
     if (total > M.npix) {
       (void)hipFree(M.d_index);
       M.d_index = nullptr;
+      M.npix = 0;
+      if (const char* e = getenv("SRR_MULTI_FAIL_INDEX"); e && atoi(e)) {  // tests: a failed allocation
+        err = "SRR_MULTI_FAIL_INDEX: the pixel index allocation fails (test hook)";
+        return SRR_ENOMEM;
+      }
       MCHK(hipMalloc((void**)&M.d_index, total * sizeof(int32_t)));
+      M.npix = total;
     }
-    M.key[0] = -1;
     MCHK(hipMemcpy(M.d_index, index.data(), total * sizeof(int32_t), hipMemcpyHostToDevice));
-    M.npix = std::max(M.npix, total);
     M.off = off;
     std::copy(key, key + 3, M.key);
   }
@@ -357,15 +385,29 @@ void merge(srr_stats& s, const srr_stats& t) {
   s.stack_overflows += t.stack_overflows;
   s.deep_traversals += t.deep_traversals;
   s.mixture_capped += t.mixture_capped;
+  s.walks_suspended += t.walks_suspended;
 }
 
-// The frame-end exchange of buffer set b once every shard has finished: the
-// shards' slabs into the packed frame on device 0 (RCCL send / recv, or
-// copies), then the scatter into d_image; returns after device 0 finished it.
-int exchange(Multi& M, int b, float* d_image, double* ms, std::string& err) {
+// The frame-end exchange of buffer set b, enqueued on the exchange streams without
+// a host wait: the shards' slabs into the packed frame on device 0 (RCCL send /
+// recv, or copies), then the scatter into d_image.  Each shard's part waits on
+// done[k] (its frame's end event; nullptr: the shard already finished on the host),
+// and device 0's part also on the caller's legacy-stream work queued before it
+// (the image's producers).  wait_exchange reads the result.
+int enqueue_exchange(Multi& M, int b, float* d_image, const std::vector<hipEvent_t>& done, std::string& err) {
   const int n = (int)M.devs.size();
   MCHK(hipSetDevice(M.devs[0]));
-  MCHK(hipEventRecord(M.ev_x0, M.xst[0]));
+  MCHK(hipEventRecord(M.ev_in[b], nullptr));
+  MCHK(hipStreamWaitEvent(M.xst[0], M.ev_in[b], 0));
+  for (int k = 0; k < n; ++k) {
+    if (!done[k]) continue;
+    // RCCL: shard k's send runs on its device's exchange stream; copies: device 0's
+    // stream reads every slab (an event of another device may be waited on)
+    MCHK(hipSetDevice(M.use_rccl ? M.devs[k] : M.devs[0]));
+    MCHK(hipStreamWaitEvent(M.use_rccl ? M.xst[k] : M.xst[0], done[k], 0));
+  }
+  MCHK(hipSetDevice(M.devs[0]));
+  MCHK(hipEventRecord(M.ev_x0[b], M.xst[0]));
   if (M.use_rccl) {
     const Rccl& R = rccl();
     ncclResult_t e = R.GroupStart();
@@ -383,6 +425,10 @@ int exchange(Multi& M, int b, float* d_image, double* ms, std::string& err) {
       err = std::string("RCCL gather: ") + R.ErrorString(e);
       return SRR_EIO;
     }
+    for (int k = 1; k < n; ++k) {  // the senders' ends (their slabs are reused by a later frame)
+      MCHK(hipSetDevice(M.devs[k]));
+      MCHK(hipEventRecord(M.ev_sent[b][k], M.xst[k]));
+    }
   } else {
     for (int k = 1; k < n; ++k) {
       const size_t bytes = 3 * (size_t)(M.off[k + 1] - M.off[k]) * sizeof(float);
@@ -393,20 +439,29 @@ int exchange(Multi& M, int b, float* d_image, double* ms, std::string& err) {
   MCHK(hipSetDevice(M.devs[0]));
   launch_scatter_pixels(M.packed[b], M.d_index, M.off[n], d_image, M.xst[0]);
   MCHK(hipGetLastError());
-  MCHK(hipEventRecord(M.ev_x1, M.xst[0]));
-  MCHK(hipStreamSynchronize(M.xst[0]));
+  MCHK(hipEventRecord(M.ev_x1[b], M.xst[0]));
+  return 0;
+}
+
+// waits for buffer set b's exchange (the host's only wait on it); its device time in *ms
+int wait_exchange(Multi& M, int b, double* ms, std::string& err) {
+  const int n = (int)M.devs.size();
+  MCHK(hipSetDevice(M.devs[0]));
+  MCHK(hipEventSynchronize(M.ev_x1[b]));
   if (M.use_rccl)
-    for (int k = 1; k < n; ++k) {  // the senders' streams (their slabs may be reused next)
+    for (int k = 1; k < n; ++k) {
       MCHK(hipSetDevice(M.devs[k]));
-      MCHK(hipStreamSynchronize(M.xst[k]));
+      MCHK(hipEventSynchronize(M.ev_sent[b][k]));
     }
+  MCHK(hipSetDevice(M.devs[0]));
   float t = 0;
-  MCHK(hipEventElapsedTime(&t, M.ev_x0, M.ev_x1));
+  MCHK(hipEventElapsedTime(&t, M.ev_x0[b], M.ev_x1[b]));
   *ms = t;
   return 0;
 }
 
-// finish the oldest frame in flight: wait for every shard, exchange, record
+// finish the oldest frame in flight: every shard's stats, then its exchange (enqueued
+// when the frame was submitted)
 int finish_oldest(Multi& M) {
   PendingFrame f = M.pending.front();
   M.pending.pop_front();
@@ -421,11 +476,14 @@ int finish_oldest(Multi& M) {
     }
     merge(d.stats, s);
   }
-  if (d.rc == 0) {
-    double ms = 0;
-    d.rc = exchange(M, f.buf, f.d_image, &ms, d.err);
-    d.stats.total_ms += ms;
+  double ms = 0;
+  std::string xerr;
+  const int xrc = wait_exchange(M, f.buf, &ms, xerr);  // (also after a shard error: the buffers are reused)
+  if (d.rc == 0 && xrc < 0) {
+    d.rc = xrc;
+    d.err = xerr;
   }
+  if (d.rc == 0) d.stats.total_ms += ms;
   M.done.push_back(d);
   return d.rc;
 }
@@ -462,7 +520,10 @@ int multi_render_device(srr_renderer* r, const srr_params* p, float* d_image, sr
     merge(s, st[k]);
   }
   double ms = 0;
-  rc = exchange(M, 0, d_image, &ms, err);
+  // (the shards finished on the host: no events to wait on)
+  rc = enqueue_exchange(M, 0, d_image, std::vector<hipEvent_t>(n, nullptr), err);
+  if (rc < 0) return rc;
+  rc = wait_exchange(M, 0, &ms, err);
   if (rc < 0) return rc;
   s.total_ms += ms;
   if (stats) *stats = s;
@@ -500,6 +561,21 @@ int multi_render_device_async(srr_renderer* r, const srr_params* p, float* d_ima
         if (f.tickets[j] >= 0) (void)srr_render_wait(M.peers[j], f.tickets[j], nullptr);
       return rc;
     }
+  }
+  // the exchange goes on the GPU now, behind each shard's frame end: the host waits
+  // for nothing until srr_render_wait
+  std::vector<hipEvent_t> done(n, nullptr);
+  for (int k = 0; k < n; ++k)
+    if (f.tickets[k] >= 0) done[k] = render_ticket_event(M.peers[k], f.tickets[k]);
+  rc = enqueue_exchange(M, f.buf, d_image, done, err);
+  if (rc < 0) {
+    for (int k = 0; k < n; ++k)
+      if (f.tickets[k] >= 0) (void)srr_render_wait(M.peers[k], f.tickets[k], nullptr);
+    for (int k = 0; k < n; ++k) {  // what was enqueued of the exchange ends before its buffers are reused
+      (void)hipSetDevice(M.devs[k]);
+      (void)hipStreamSynchronize(M.xst[k]);
+    }
+    return rc;
   }
   M.next_ticket++;
   M.pending.push_back(f);

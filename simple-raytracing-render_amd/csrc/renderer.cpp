@@ -409,10 +409,18 @@ static int paths_enqueue(srr_renderer* r, FrameSlot& F, const srr_params* p, boo
   // (SRR_GSTACK=0 disables it: every deeper traversal then re-walks the BVH2)
   const char* gs_env = getenv("SRR_GSTACK");
   const int gst_cap = (r->has_meshes && !(gs_env && !atoi(gs_env))) ? kPathsGlobalStack : 0;
-  if (gst_cap && !F.gstack) RCHK(hipMalloc((void**)&F.gstack, (size_t)gst_cap * r->pw_lanes * sizeof(int2)));
+  // ... followed by the save area of suspended mesh walks (3 float4 per lane)
+  if (gst_cap && !F.gstack)
+    RCHK(hipMalloc((void**)&F.gstack, (size_t)gst_cap * r->pw_lanes * sizeof(int2) + 3 * (size_t)r->pw_lanes * sizeof(float4)));
+  // suspendable mesh walks: a walk still running when at most SRR_WALK_Q / 64
+  // of its wave's lanes walk (default 8) continues in the next wave-iteration; SRR_WALK_Q=0
+  // never suspends (read per frame: tests switch it between renders)
+  const char* wq_env = getenv("SRR_WALK_Q");
+  const int walk_q = wq_env ? std::max(0, std::min(64, atoi(wq_env))) : 8;
   // sample window: all pixels x W samples, buffer within SRR_WINDOW_MB (default 8192)
   size_t budget = (size_t)8192 << 20;
   if (const char* e = getenv("SRR_WINDOW_MB")) budget = (size_t)std::max(1, atoi(e)) << 20;
+  budget /= (size_t)std::max(1, r->window_share);
   // (k_paths numbers a window's paths in 32 bits: npix * W < 2^31)
   const int64_t w_max = std::max<int64_t>(1, (((int64_t)1 << 31) - 1) / std::max<int64_t>(1, npix));
   const int W = (int)std::max<int64_t>(
@@ -505,12 +513,17 @@ static int paths_enqueue(srr_renderer* r, FrameSlot& F, const srr_params* p, boo
     w.gstack_cap = gst_cap;
     w.wave_times = wave_times;
     w.deep_tries = deep_tries;
+    w.walk_q = gst_cap ? walk_q : 0;  // (the save area follows the global stack extension)
     w.slow_rays = diagnostics ? r->pw_slow : nullptr;
     w.slow_count = w.slow_rays ? (unsigned*)(r->pw_slow + 16 * 65536) : nullptr;
     const int wi = s0 / W;
     if (wi > 0) RCHK(hipMemsetAsync(w.cursor, 0, sizeof(unsigned long long), st));  // window 0: zeroed with ctr
     RCHK(hipEventRecord(F.win_ev[2 * wi], st));
-    launch_paths(r->view, w, all_fam ? 1 : 0, st);
+    if (launch_paths(r->view, w, all_fam ? 1 : 0, st) != 0) {
+      err = "k_paths refused: stack_cap " + std::to_string(w.stack_cap) +
+            " exceeds the kernel build's LDS stack (a host and kernels built with different SRR_KSTACK)";
+      return SRR_EINVAL;
+    }
     RCHK(hipEventRecord(F.win_ev[2 * wi + 1], st));
     // the last window also writes the output (k_finish fused): means, or raw sums (SRR_FLAG_SUMS)
     const bool last = s0 + Wn >= p->spp;
@@ -590,6 +603,7 @@ static int paths_finish(srr_renderer* r, FrameSlot& F, const srr_params* p, srr_
             ctr[31] / it, ctr[32] / it, ctr[33] / it);
     fprintf(stderr, "  beckmann mixture: %.2f attempts per Beckmann scatter, %.2f for the wave's slowest lane per run\n",
             per(ctr[34], ctr[22]), per(ctr[35], ctr[19]));
+    fprintf(stderr, "  suspended walks: %.2f lanes per wave-iteration\n", ctr[36] / it);
   }
 #ifdef SRR_SLOW_RAYS
   if (r->pw_slow) {  // diagnostics build: dump the slow world hits' records (one line per lane, JSON)
@@ -621,6 +635,7 @@ static int paths_finish(srr_renderer* r, FrameSlot& F, const srr_params* p, srr_
   s.stack_overflows = (int64_t)ctr[11];
   s.deep_traversals = (int64_t)ctr[12];
   s.mixture_capped = (int64_t)ctr[15];
+  s.walks_suspended = (int64_t)ctr[36];
   s.paths = F.paths;
   s.trace_ms = kernel_ms;
   s.total_ms = total;
@@ -752,6 +767,12 @@ int render_device_async(srr_renderer* r, const srr_params* p, const int32_t* pix
   F.busy = true;
   *ticket = F.ticket;
   return 0;
+}
+
+hipEvent_t render_ticket_event(srr_renderer* r, int64_t ticket) {
+  for (FrameSlot& F : r->async_slots)
+    if (F.busy && F.ticket == ticket) return F.ev_end;
+  return nullptr;
 }
 
 int render_wait(srr_renderer* r, int64_t ticket, srr_stats* stats, std::string& err) {

@@ -56,7 +56,9 @@ struct FrameSlot {
   std::vector<hipEvent_t> win_ev;  // per sample window: k_paths start / end
   float4* rec = nullptr;
   size_t rec_cap = 0;
-  int2* gstack = nullptr;  // [kPathsGlobalStack][pw_lanes] (kernels.h)
+  // [kPathsGlobalStack][pw_lanes] int2 (kernels.h), then [3][pw_lanes] float4 of suspended
+  // mesh walks (kernels.h PathWork::walk_q)
+  int2* gstack = nullptr;
   float* sample = nullptr;
   size_t sample_cap = 0;
   unsigned long long* ctr = nullptr;       // [0] world rays, [1] path cursor, ...
@@ -111,6 +113,9 @@ struct srr_renderer {
   int64_t next_ticket = 0;
   std::vector<srr::DoneTicket> done_tickets;
   hipEvent_t ev_async_in = nullptr;  // orders an async frame after the caller's legacy-stream work
+  // renderers sharing this device under one multi-device handle (multi.cpp): each takes
+  // 1/window_share of the sample-window budget (SRR_WINDOW_MB)
+  int window_share = 1;
   unsigned long long* pw_wave_times = nullptr;  // SRR_WAVE_TIMES diagnostics, 4 words per wave
   float* pw_slow = nullptr;  // diagnostics build (-DSRR_SLOW_RAYS): slow world-hit records + count
   int32_t* pixels = nullptr;
@@ -143,4 +148,7 @@ int render_device_async(srr_renderer* r, const srr_params* p, const int32_t* pix
                         int64_t* ticket, std::string& err);
 int render_wait(srr_renderer* r, int64_t ticket, srr_stats* stats, std::string& err);
 void drain_async(srr_renderer* r);  // finish every async frame in flight (results kept for render_wait)
+// the event recorded after async frame `ticket`'s last operation (its slot's frame end),
+// or nullptr when that frame is no longer in flight (multi.cpp orders its exchange by it)
+hipEvent_t render_ticket_event(srr_renderer* r, int64_t ticket);
 }  // namespace srr

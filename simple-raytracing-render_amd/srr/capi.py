@@ -37,7 +37,7 @@ class Stats(ctypes.Structure):
                 ("trace_ms", ctypes.c_double), ("shade_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
                 ("bounces", ctypes.c_int64), ("box_tests", ctypes.c_int64), ("tri_tests", ctypes.c_int64),
                 ("stack_overflows", ctypes.c_int64), ("deep_traversals", ctypes.c_int64),
-                ("mixture_capped", ctypes.c_int64)]
+                ("mixture_capped", ctypes.c_int64), ("walks_suspended", ctypes.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

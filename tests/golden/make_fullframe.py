@@ -51,6 +51,10 @@ FRAMES = {
     "c4_full": (lambda: scenes.s4_soldier_standin()[0].text(), 1920, 1080, 16, 50, 16),
     "c5_full": (lambda: scenes.s5_soldier_fog()[0].text(), 1920, 1080, 16, 50, 16),
     "c4r_full": (soldier_fixture.scene_text, 1920, 1080, 16, 50, 16),
+    # C3 (the microfacet teapot, Raytracing_n.cpp:324, and the dielectric sphere) and its
+    # metal variant (:348): whole 512x512x1024 frames, per pixel
+    "c3_full": (lambda: scenes.s3_cornell_teapot_microfacet()[0].text(), 512, 512, 1024, 50, 0),
+    "c3m_full": (lambda: scenes.s3_cornell_teapot_microfacet("metal")[0].text(), 512, 512, 1024, 50, 0),
 }
 
 

@@ -29,6 +29,7 @@ def contents_dir() -> str:
     import lzma
     global _CONTENTS
     if _CONTENTS is None:
+        soldier_fixture.require(ASSETS)
         d = tempfile.mkdtemp(prefix="srr_contents_")
         z = np.load(ASSETS)  # plain arrays only (allow_pickle stays False)
         for k in z.files:
@@ -51,6 +52,7 @@ def scene_text(key: str) -> str:
         from srr import ref_scenes
         m = json.load(open(os.path.join(os.path.dirname(FIXTURE), "ref_scenes.json")))[key]
         return ref_scenes.BUILDERS[m["builder"]](m["nx"] / m["ny"], contents_dir(), **m["kwargs"]).text()
+    soldier_fixture.require(FIXTURE)
     z = np.load(FIXTURE)  # plain arrays only (allow_pickle stays False)
     if key == "reft_soldier_scene":
         cam = z["camera_reft_soldier_scene"].tobytes().decode()

@@ -88,3 +88,44 @@ def test_1080p_full_frame_is_the_reference_frame(name):
         _save_diag(name, (bad_groups[:, None] * g + np.arange(g)[None, :]).ravel(), out)
     assert out["stats"]["world_rays"] == m["world_rays"], res
     assert res["ray_mismatch_groups"] == 0 and res["hash_mismatch_groups"] == 0, res
+
+
+@pytest.mark.parametrize("name", ["c3_full", "c3m_full"])
+def test_c3_full_frame_is_the_reference_frame(name):
+    """C3's WHOLE 512x512x1024 frame (268 M paths): the microfacet teapot
+    (beckmann 0.01 / 0.05, Raytracing_n.cpp:324, material.h:151-199,
+    microfacet_distribution.h) and the dielectric sphere (material.h:282-325), and
+    the metal-teapot variant (:348); per-pixel world rays, path hashes and means
+    against the reference's own render (tests/golden/make_fullframe.py)."""
+    m = fullframe.meta(name)
+    want = fullframe.load(name)
+    out = capi.Renderer(fullframe.scene_text(name)).render(m["nx"], m["ny"], m["spp"], m["max_depth"], keep_paths=True)
+    got = fullframe.digest(out["paths"], out["rays"])
+    got["mean"] = out["mean"]
+    res = fullframe.compare(got, want)
+    res["stats_world_rays"] = out["stats"]["world_rays"]
+    print(name, res)
+    _save_diag(name, np.flatnonzero((got["hash"] != want["hash"]) | (got["rays"] != want["rays"])), out)
+    assert out["stats"]["world_rays"] == m["world_rays"], res
+    assert res["ray_mismatch_pixels"] == 0 and res["hash_mismatch_pixels"] == 0, res
+    assert res["mean_mismatch_pixels"] == 0, res
+
+
+@pytest.mark.parametrize("name", ["c4_full", "c4r_full"])
+def test_1080p_sample_windows_are_the_reference_frame(name, monkeypatch):
+    """A 1080p frame cut into sample windows (renderer.cpp paths_enqueue: a window
+    holds as many samples of every pixel as SRR_WINDOW_MB allows; the bench's C4
+    frame runs 3 per frame): SRR_WINDOW_MB=150 gives windows of 6, 6 and 4 of the
+    16 samples, so each pixel's paths come from three k_paths launches and are summed
+    across two window boundaries -- every path and every pixel group still the
+    reference's."""
+    monkeypatch.setenv("SRR_WINDOW_MB", "150")
+    m = fullframe.meta(name)
+    want = fullframe.load(name)
+    out = capi.Renderer(fullframe.scene_text(name)).render(m["nx"], m["ny"], m["spp"], m["max_depth"], keep_paths=True)
+    assert out["stats"]["trace_launches"] == 3, out["stats"]
+    got = fullframe.digest(out["paths"], out["rays"])
+    res = fullframe.compare(got, want)
+    print(name, "windows", res)
+    assert out["stats"]["world_rays"] == m["world_rays"], res
+    assert res["ray_mismatch_groups"] == 0 and res["hash_mismatch_groups"] == 0, res

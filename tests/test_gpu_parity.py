@@ -257,3 +257,34 @@ def test_stack_overflow_rewalk_matches_reference(name, gstack, quad, monkeypatch
     assert pc["bitexact"] >= parity.MIN_BITEXACT, pc
     assert (out["rays"] == gr).all()
     assert out["stats"]["world_rays"] == m["world_rays"]
+
+
+@pytest.mark.parametrize("walk", [("0", "0"), ("64", "0"), ("64", "2"), ("8", "0"), ("24", "0")])
+@pytest.mark.parametrize("name", ["s2", "s3", "s4_d40", "s5_d40", "s2_d100"])
+def test_suspended_walks_match_reference(name, walk, monkeypatch):
+    """Suspendable mesh walks (kernels.hip TraceCtx::walk_thr, DESIGN §5.1): a walk
+    may stop part-way and continue in a later wave-iteration from its saved state
+    (next node, stack top and depth, best hit, bound; the list's object and
+    closest-so-far).  SRR_WALK_Q=64 suspends every walk after each node step -- the
+    most resumes the kernel can make -- and with SRR_STACK_CAP=2 the suspended
+    stacks also reach into the global extension; SRR_WALK_Q=0 never suspends.
+    Every path bit-identical to the reference's, the same world rays, and the
+    counter shows the walks suspended."""
+    q, cap = walk
+    m, text, gp, gr, gi = golden(name)
+    monkeypatch.setenv("SRR_WALK_Q", q)
+    if cap != "0":
+        monkeypatch.setenv("SRR_STACK_CAP", cap)
+    out = capi.Renderer(text).render(m["nx"], m["ny"], m["spp"], m["max_depth"], keep_paths=True)
+    pc = parity.compare_paths(out["paths"], gp)
+    st = out["stats"]
+    print(name, walk, pc, "suspended:", st["walks_suspended"], "deep:", st["deep_traversals"])
+    if q == "0":
+        assert st["walks_suspended"] == 0
+    elif q == "64":
+        assert st["walks_suspended"] > 0
+    if cap != "0" and name != "s2":
+        assert st["deep_traversals"] > 0
+    assert pc["bitexact"] >= parity.MIN_BITEXACT, pc
+    assert (out["rays"] == gr).all()
+    assert st["world_rays"] == m["world_rays"]

@@ -122,3 +122,49 @@ def test_multi_refuses_kept_paths_and_forced_rccl_on_a_repeated_device(monkeypat
     with pytest.raises(capi.SrrError, match="distinct devices"):
         capi.Renderer(sc.text(), devices=[0, 0])
     assert os.environ["SRR_MULTI_TRANSPORT"] == "rccl"
+
+
+@pytest.mark.gpu
+def test_multi_fewer_pixels_than_devices_orders_the_scatter_after_the_callers_fill():
+    """A frame with fewer pixels than shards (the last shard empty): the gather
+    and scatter into the caller's image run after the caller's own work on it --
+    here a fill of the image queued on the legacy stream right before the async
+    render -- because device 0's exchange stream waits on that stream, not on any
+    shard's frame: the image is the frame, not the fill."""
+    import torch
+    sc, _ = scenes.s1_cornell()
+    text = sc.text()
+    nx, ny, spp = 2, 1, 4
+    want, _ = _frame(capi.Renderer(text, device=0), nx, ny, spp, 1)
+    m = capi.Renderer(text, devices=[0, 0, 0])
+    p = capi.make_params(nx, ny, spp, 50, tile=1)
+    for _ in range(3):
+        buf = torch.empty((nx * ny, 3), dtype=torch.float32, device="cuda")
+        buf.fill_(7.0)
+        t = m.render_device_async(p, buf.data_ptr())
+        m.wait(t)
+        np.testing.assert_array_equal(buf.cpu().numpy().view(np.uint32), want[0].view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_multi_failed_index_allocation_leaves_no_stale_plan(monkeypatch):
+    """The gather's pixel index is reallocated when a larger frame arrives; if that
+    allocation fails (SRR_MULTI_FAIL_INDEX test hook), the renderer must not keep
+    the old plan's key with a freed index: rendering the old size again restages
+    and is bitwise the one-device frame."""
+    sc, _ = scenes.s1_cornell()
+    text = sc.text()
+    m = capi.Renderer(text, devices=[0, 0])
+    small, big = (24, 16), (40, 32)
+    want, _ = _frame(capi.Renderer(text, device=0), *small, 4, 1)
+    got, _ = _frame(m, *small, 4, 1)
+    np.testing.assert_array_equal(got[0].view(np.uint32), want[0].view(np.uint32))
+    monkeypatch.setenv("SRR_MULTI_FAIL_INDEX", "1")
+    with pytest.raises(capi.SrrError, match="SRR_MULTI_FAIL_INDEX"):
+        _frame(m, *big, 4, 1)
+    monkeypatch.delenv("SRR_MULTI_FAIL_INDEX")
+    got, _ = _frame(m, *small, 4, 1)
+    np.testing.assert_array_equal(got[0].view(np.uint32), want[0].view(np.uint32))
+    wbig, _ = _frame(capi.Renderer(text, device=0), *big, 4, 1)
+    got, _ = _frame(m, *big, 4, 1)
+    np.testing.assert_array_equal(got[0].view(np.uint32), wbig[0].view(np.uint32))

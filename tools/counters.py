@@ -10,7 +10,9 @@ and tallies 64 B per 128-B request on gfx950 (doubled); WRITE_SIZE is KiB.
 import collections
 import csv
 import glob
+import hashlib
 import json
+import os
 import sys
 
 N_CU = 256
@@ -67,7 +69,20 @@ def main():
             out["world_rays_per_launch"] = round(b["config"]["world_rays_per_step"] * b["steps"] / launches)
             out["profiled_workload"] = b["config"]["workload"]
             break
+    # the build these counters describe: bench.py prices a summary only on the same library
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.environ.get("SRR_LIB") or os.path.join(root, "simple-raytracing-render_amd", "libsrr.so")
+    out["build"] = {"lib": os.path.relpath(lib, root), "lib_sha256": lib_sha256(lib),
+                    "env": {k: v for k, v in sorted(os.environ.items()) if k.startswith("SRR_")}}
     print(json.dumps(out, indent=1))
+
+
+def lib_sha256(path):
+    """first 16 hex digits of the library's SHA-256 (bench.py compares them)"""
+    try:
+        return hashlib.sha256(open(path, "rb").read()).hexdigest()[:16]
+    except OSError:
+        return None
 
 
 if __name__ == "__main__":
