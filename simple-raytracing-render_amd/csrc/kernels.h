@@ -27,7 +27,7 @@ struct SceneView {  // device pointers into the flattened tables (device_scene.h
   int use_q;            // k_paths traces meshes over node4q (SRR_CBVH)
   int quad_trace;       // k_paths traces meshes quad-cooperatively (BVH4 larger than an XCD's L2)
   int quad_max;         // ...when at most this many lanes of the wave enter the mesh (else per lane)
-  int mesh_obj;         // the world list's one top-level mesh object (k_paths CMP variant), else -1
+  int mesh_obj;         // the world list's one top-level mesh object, else -1 (kernels.hip world_hit: walk suspension's list mode)
   const float4* tri_pos;  // 4 float4 per triangle: p0, p1, p2, pad
   const float4* tri_edge;  // 8 float4 per triangle i: p0, e1, e2 of i and i+1 packed (renderer.cpp)
   const TriShade* tri_shade;

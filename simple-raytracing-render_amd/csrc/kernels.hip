@@ -309,6 +309,7 @@ struct TraceCtx {
   int walk_thr = -1;
   mutable int resume = 0;
   mutable int susp = 0;
+  mutable int obj_k = -1;  // (SUSP) the world-list object under test (set by world_hit; wave-uniform)
   // SRR_TIMING diagnostics (wave-uniform): cycles inside mesh traversals, steps
   mutable uint64_t mesh_cycles = 0;
   mutable int mesh_steps = 0;       // node steps of the wave's longest walk
@@ -524,20 +525,23 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
   float top_t = 0.f;
 #endif
   if constexpr (SUSP) {
-    if (cx.resume) {  // the walk this lane suspended in an earlier wave-iteration
-      const float4 a = *walk_save(cx, 0), b = *walk_save(cx, 1);
-      node = __float_as_int(a.x);
-      sp = __float_as_int(a.y);
-      top_n = __float_as_int(a.z);
-      top_t = a.w;
-      best_t = b.x;
-      best_i = __float_as_int(b.y);
-      found = best_i >= 0;
-      bound = b.z;
+    if (cx.resume) {  // the walk this lane suspended in an earlier wave-iteration, if it is this object's
+      const float4 b = *walk_save(cx, 1);
       const int fl = __float_as_int(b.w);
-      overflow = (fl & 1) != 0;
-      deep = (fl & 2) != 0;
-      cx.resume = 0;
+      if ((fl >> 2) == cx.obj_k) {
+        const float4 a = *walk_save(cx, 0);
+        node = __float_as_int(a.x);
+        sp = __float_as_int(a.y);
+        top_n = __float_as_int(a.z);
+        top_t = a.w;
+        best_t = b.x;
+        best_i = __float_as_int(b.y);
+        found = best_i >= 0;
+        bound = b.z;
+        overflow = (fl & 1) != 0;
+        deep = (fl & 2) != 0;
+        cx.resume = 0;
+      }
     }
   }
   for (;;) {
@@ -907,8 +911,8 @@ SRR_D bool mesh_hit4(const SceneView& S, const DMesh& m, const Ray& r, float tmi
   if constexpr (SUSP) {
     if (node >= 0) {  // stopped with a next node: the walk's state at the top of that step
       *walk_save(cx, 0) = make_float4(__int_as_float(node), __int_as_float(sp), __int_as_float(top_n), top_t);
-      *walk_save(cx, 1) =
-          make_float4(best_t, __int_as_float(best_i), bound, __int_as_float((overflow ? 1 : 0) | (deep ? 2 : 0)));
+      *walk_save(cx, 1) = make_float4(best_t, __int_as_float(best_i), bound,
+                                      __int_as_float((overflow ? 1 : 0) | (deep ? 2 : 0) | (cx.obj_k << 2)));
       cx.susp = 1;
       suspended = true;
     }
@@ -980,9 +984,6 @@ constexpr int TR_Q = 64;  // meshes traced over the compressed 64-B nodes (Scene
 constexpr int TR_BIG = 128;  // the 1,024-lane path kernel: LDS stacks with stride 1,024
 constexpr int tr_stride(int tr) { return (tr & TR_BIG) ? 1024 : kTraceBlock; }
 constexpr int TR_SUSP = 256;  // the path kernel: mesh walks may suspend and resume (TraceCtx::walk_thr)
-#ifndef SRR_SUSP
-#define SRR_SUSP 1  // (A/B: -DSRR_SUSP=0 builds k_paths without suspendable walks)
-#endif
 
 template <int CTRL>
 SRR_D int quad_dpp(int x) { return __builtin_amdgcn_update_dpp(x, x, CTRL, 0xF, 0xF, false); }
@@ -1580,20 +1581,29 @@ SRR_D void world_objs(const SceneView& S, const Ray& r, Rng& rng, const TraceCtx
   }
 }
 
-// TR_SUSP: a lane's mesh walk may suspend (cx.susp): the lane leaves the list
-// there, its list state (object, closest-so-far, record so far) saved beside the
-// walk's; a resuming lane (cx.resume) restores it, passes over the objects before
-// its mesh (their tests are done) and continues the walk, then the list.  The
-// objects stay in list order for every lane, so the result is the same.
+// TR_SUSP: a lane's mesh walk may suspend (cx.susp) and its world hit is then
+// redone in a later wave-iteration (cx.resume), the walk continuing from its saved
+// state at the same object (cx.obj_k).  With one mesh in the list and no media
+// (SceneView::mesh_obj >= 0) the objects before the mesh are simply tested again --
+// pure functions of the ray and the closest-so-far, the same results -- and the
+// objects a suspended lane meets after its mesh are tested for nothing (the wave
+// tests them for its other lanes anyway; k_paths discards the suspended lane's
+// result).  Otherwise ("skip" mode) the list state (object, closest-so-far, record so
+// far) is saved beside the walk's, a resuming lane passes over the objects before
+// its mesh and a suspended lane over the objects after it: a medium draws from the
+// path's RNG (constant_medium.h:19-50), which must not be drawn twice, and another
+// mesh walk would reuse the lane's traversal stack, which holds the suspended walk.
+// The objects stay in list order for every lane, so the result is the same.
 template <bool MEDIA, int TR>
 SRR_D WorldHit world_hit(const SceneView& S, const Ray& r, Rng& rng, const TraceCtx& cx) {
   WorldHit w{-1, -1, 0};
   float closest = FLT_MAX;  // numeric_limits<float>::max(), Raytracing_n.cpp:58
   const float tmin = 0.001f;
   constexpr bool SUSP = (TR & TR_SUSP) != 0;
-  int k_res = -1;  // (SUSP) the object whose walk this lane resumes
+  const bool skip = MEDIA || S.mesh_obj < 0;  // (wave-uniform) the list state is saved, see above
+  int k_res = -1;  // (SUSP, skip) the object whose walk this lane resumes
   if constexpr (SUSP) {
-    if (cx.resume) {
+    if (skip && cx.resume) {
       const float4 v = *walk_save(cx, 2);
       k_res = __float_as_int(v.x);
       closest = v.y;
@@ -1604,8 +1614,11 @@ SRR_D WorldHit world_hit(const SceneView& S, const Ray& r, Rng& rng, const Trace
   }
   for (int k = 0; k < S.n_world; ++k) {
     const DObj ob = maybe_uni<SRR_UNIFORM != 0>(wload<TR>(S.objs, k));
-    // (a per-lane skip, not a break: the object loop stays wave-uniform)
-    if (SUSP && (cx.susp || k < k_res)) continue;
+    if constexpr (SUSP) {
+      // (a per-lane skip, not a break: the object loop stays wave-uniform)
+      if (skip && (cx.susp || k < k_res)) continue;
+      cx.obj_k = k;
+    }
     Ray lr = chain_in<TR, SRR_UNIFORM != 0>(S, ob, r);
     ObjHit h;
     bool hit;
@@ -1615,7 +1628,7 @@ SRR_D WorldHit world_hit(const SceneView& S, const Ray& r, Rng& rng, const Trace
     } else {
       hit = basic_hit<TR, SRR_UNIFORM != 0>(S, ob, lr, tmin, closest, false, h, cx);
     }
-    if (SUSP && cx.susp) {
+    if (SUSP && skip && cx.susp) {
       *walk_save(cx, 2) = make_float4(__int_as_float(k), closest, __int_as_float(w.obj), __int_as_float(w.prim));
       continue;
     }
@@ -3120,8 +3133,10 @@ SRR_D kptr<PathsArgs> paths_args() {
 SRR_D const PathsArgs* paths_args() { return nullptr; }
 #endif
 
+// SP: mesh walks may suspend (TR_SUSP; launched when PathWork::walk_q > 0): the 1,024-lane
+// variants and the diagnostics (TIMED) one are built both ways
 template <bool MEDIA, bool ALLFAM, int MINB, bool TIMED = false, bool WL = true, bool QUAD = false, bool CQ = false,
-          int BS = kPathsBlock>
+          int BS = kPathsBlock, bool SP = false>
 #ifdef SRR_NUM_VGPR  // register-pressure study builds only: cap k_paths' VGPRs
 #define SRR_PATHS_VGPR_ATTR __attribute__((amdgpu_num_vgpr(SRR_NUM_VGPR)))
 #else
@@ -3143,7 +3158,7 @@ __global__ void __launch_bounds__(BS, MINB) SRR_PATHS_VGPR_ATTR k_paths(PathsArg
   // QUAD: meshes traced by mesh_hit4_quad (large BVHs, SceneView::quad_trace)
   // (per-lane walks over 128-B nodes may suspend: TR_SUSP, PathWork::walk_q)
   constexpr int TR = TR_BVH4_PRUNE | (WL ? TR_WL : 0) | (QUAD ? TR_QUAD : 0) | (CQ ? TR_Q : 0) | (BS == 1024 ? TR_BIG : 0) |
-                     ((QUAD || CQ || !SRR_SUSP) ? 0 : TR_SUSP);
+                     ((SP && !QUAD && !CQ) ? TR_SUSP : 0);
   __shared__ uint4 s_world[WL ? kWorldLdsBytes / 16 : 1];
   // the scene as a phase reads it: scalar loads of the fields it uses, the world
   // tables re-pointed into LDS (WL)
@@ -3357,7 +3372,7 @@ __global__ void __launch_bounds__(BS, MINB) SRR_PATHS_VGPR_ATTR k_paths(PathsArg
       cx.last_steps = 0;
       const Ray r_in = r;
 #endif
-      w = world_hit<MEDIA, TIMED ? (TR_BVH4_TIMED | (WL ? TR_WL : 0) | TR_SUSP) : TR>(S, r, rng, cx);
+      w = world_hit<MEDIA, TIMED ? (TR_BVH4_TIMED | (WL ? TR_WL : 0) | (SP ? TR_SUSP : 0)) : TR>(S, r, rng, cx);
       if constexpr ((TR & TR_SUSP) != 0) {
         walking = cx.susp;  // (its record, scatter and fold wait for the walk's end)
         if (walking) {
@@ -4213,12 +4228,16 @@ int launch_paths(const SceneView& S, const PathWork& W, int all_families, hipStr
   }
   const int bs = paths_block_lanes(S);
   const int blocks_b = W.lanes / bs;
+  // suspendable mesh walks: the variant with them when the frame asks for them (walk_q > 0);
+  // only the 1,024-lane (mesh scene) and diagnostics variants have one
+  const bool sp = W.walk_q > 0;
 #if SRR_DIAG_VARIANTS
   // diagnostics build (make diag): SRR_PATHS_TIMING=1 phase timing, SRR_CBVH=1 compressed nodes
   static const bool timed = getenv("SRR_PATHS_TIMING") != nullptr;
   const bool cq = S.use_q && !S.quad_trace && !timed;  // compressed nodes, per-lane walks
 #define SRR_LAUNCH_PATHS_DIAG(M, A, B)                                                                                         \
-  if (timed) hipLaunchKernelGGL((dev::k_paths<M, A, 4, true>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, args);           \
+  if (timed && sp) hipLaunchKernelGGL((dev::k_paths<M, A, 4, true, true, false, false, dev::kPathsBlock, true>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, args); \
+  else if (timed) hipLaunchKernelGGL((dev::k_paths<M, A, 4, true>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, args);      \
   else if (bs == 1024 && B == 4 && cq) hipLaunchKernelGGL((dev::k_paths<M, A, 4, false, true, false, true, 1024>), dim3(blocks_b), dim3(1024), 0, st, args); \
   else if (cq && B == 4) hipLaunchKernelGGL((dev::k_paths<M, A, 4, false, true, false, true>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, args); \
   else
@@ -4229,7 +4248,8 @@ int launch_paths(const SceneView& S, const PathWork& W, int all_families, hipStr
 #endif
 #define SRR_LAUNCH_PATHS(M, A, B)                                                                      \
   SRR_LAUNCH_PATHS_DIAG(M, A, B)                                                                       \
-  if (bs == 1024 && B == 4 && !S.quad_trace) hipLaunchKernelGGL((dev::k_paths<M, A, 4, false, true, false, false, 1024>), dim3(blocks_b), dim3(1024), 0, st, args); \
+  if (bs == 1024 && B == 4 && !S.quad_trace && sp) hipLaunchKernelGGL((dev::k_paths<M, A, 4, false, true, false, false, 1024, true>), dim3(blocks_b), dim3(1024), 0, st, args); \
+  else if (bs == 1024 && B == 4 && !S.quad_trace) hipLaunchKernelGGL((dev::k_paths<M, A, 4, false, true, false, false, 1024>), dim3(blocks_b), dim3(1024), 0, st, args); \
   else if (S.quad_trace && B == 4) hipLaunchKernelGGL((dev::k_paths<M, A, 4, false, true, true>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, args); \
   else hipLaunchKernelGGL((dev::k_paths<M, A, B>), dim3(blocks), dim3(dev::kPathsBlock), 0, st, args)
 #ifdef SRR_OCC_VARIANTS  // occupancy A/B builds (SRR_PATHS_OCC): 2, 3, 5 and 6 blocks per CU

@@ -183,6 +183,16 @@ int renderer_create_flat(const Flat& F, int device, srr_renderer** out, std::str
   r->diffuse_only = true;
   for (const DMat& m : F.mats)
     if (m.kind != MAT_LAMBERTIAN && m.kind != MAT_ORENNAYAR && m.kind != MAT_DIFFUSE_LIGHT) r->diffuse_only = false;
+  // suspendable mesh walks by default (SRR_WALK_Q unset) where they were
+  // measured to pay: specular / microfacet materials or media (walks from surfaces inside
+  // the mesh's box run long: C3 +2 %, C4 +4 %, C4_real +3 %, C5 +6 %) or a large mesh (the
+  // 640,000-triangle teapot +3 %); not for a diffuse-only scene with a small mesh, whose
+  // walks are short (C2: the suspension check costs 0.5-1 % and gains nothing)
+  {
+    int max_tris = 0;
+    for (const DMesh& m : F.meshes) max_tris = std::max(max_tris, (int)m.n_tris);
+    r->walk_q_default = (!F.meshes.empty() && (!r->diffuse_only || V.has_media || max_tris >= 20000)) ? 8 : 0;
+  }
   RCHK(hipStreamCreateWithFlags(&r->acc_st, hipStreamNonBlocking));
   RCHK(hipEventCreate(&r->ev_beg));
   RCHK(hipEventCreate(&r->ev_end));
@@ -413,10 +423,11 @@ static int paths_enqueue(srr_renderer* r, FrameSlot& F, const srr_params* p, boo
   if (gst_cap && !F.gstack)
     RCHK(hipMalloc((void**)&F.gstack, (size_t)gst_cap * r->pw_lanes * sizeof(int2) + 3 * (size_t)r->pw_lanes * sizeof(float4)));
   // suspendable mesh walks: a walk still running when at most SRR_WALK_Q / 64
-  // of its wave's lanes walk (default 8) continues in the next wave-iteration; SRR_WALK_Q=0
-  // never suspends (read per frame: tests switch it between renders)
+  // of its wave's lanes walk continues in the next wave-iteration (default: the scene's
+  // walk_q_default, 8 or 0); SRR_WALK_Q=0 never suspends and launches the kernel variant
+  // without the feature (read per frame: tests switch it between renders)
   const char* wq_env = getenv("SRR_WALK_Q");
-  const int walk_q = wq_env ? std::max(0, std::min(64, atoi(wq_env))) : 8;
+  const int walk_q = wq_env ? std::max(0, std::min(64, atoi(wq_env))) : r->walk_q_default;
   // sample window: all pixels x W samples, buffer within SRR_WINDOW_MB (default 8192)
   size_t budget = (size_t)8192 << 20;
   if (const char* e = getenv("SRR_WINDOW_MB")) budget = (size_t)std::max(1, atoi(e)) << 20;

@@ -107,6 +107,7 @@ struct srr_renderer {
   // path-resident engine (render_paths)
   int pw_lanes = 0;
   bool diffuse_only = false;  // no beckmann / specular materials: lean kernel variant
+  int walk_q_default = 0;     // suspendable mesh walks unless SRR_WALK_Q says otherwise (renderer.cpp)
   bool has_meshes = false;
   srr::FrameSlot sync_slot;         // srr_render_device (stream acc_st, sums in acc)
   srr::FrameSlot async_slots[2];    // srr_render_device_async, alternating

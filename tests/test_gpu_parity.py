@@ -288,3 +288,46 @@ def test_suspended_walks_match_reference(name, walk, monkeypatch):
     assert pc["bitexact"] >= parity.MIN_BITEXACT, pc
     assert (out["rays"] == gr).all()
     assert st["world_rays"] == m["world_rays"]
+
+
+def _multi_mesh_scene(fog: bool):
+    """Cornell box with three meshes in the world list: one teapot BVH placed twice
+    (two instances of the same mesh, different transforms) and a second teapot mesh;
+    with fog, a constant_medium ahead of them in the list (its RNG draws must not be
+    repeated when a walk resumes)."""
+    from srr.scene import Scene
+    sc = Scene()
+    objs, white = scenes._cornell(sc)
+    if fog:
+        objs.insert(0, sc.constant_medium(sc.sphere((278, 278, 278), 2000, white), 0.0004,
+                                          sc.constant_texture((1.0, 1.0, 1.0))))
+    metal = sc.metal(0.9, 0.0)
+    shared = sc.bvh_node(sc.teapot(45.0, 6, metal), 0, 1)
+    objs.append(sc.translate(sc.rotate_x(shared, 90), (360, 0, 330)))
+    objs.append(sc.translate(sc.rotate_x(shared, 90), (170, 180, 300)))
+    objs.append(scenes._teapot_instance(sc, white, 5, scale=35.0, at=(300, 300, 200)))
+    sc.set_world(sc.hitable_list(objs))
+    scenes._cornell_camera_and_lights(sc)
+    return sc
+
+
+@pytest.mark.parametrize("fog", [False, True])
+def test_suspended_walks_with_several_meshes_match_oracle(fog, monkeypatch):
+    """Walk suspension with several meshes in one world list (kernels.hip world_hit:
+    a walk resumes at the object it stopped in, TraceCtx::obj_k; a lane suspended in
+    one mesh does not start a later one) and with a medium in the list (the
+    list-state save, so the medium's draws are not repeated): every path of the most
+    resuming setting (SRR_WALK_Q=64) and of the plain one (0) bit-identical to the
+    CPU restatement."""
+    text = _multi_mesh_scene(fog).text()
+    nx, ny, spp = 24, 24, 8
+    ref = ob.render(text, nx, ny, spp, 50, threads=8)
+    for q in ("64", "0"):
+        monkeypatch.setenv("SRR_WALK_Q", q)
+        out = capi.Renderer(text).render(nx, ny, spp, 50, keep_paths=True)
+        pc = parity.compare_paths(out["paths"], ref["paths"])
+        print("multi-mesh fog" if fog else "multi-mesh", q, pc, "suspended", out["stats"]["walks_suspended"])
+        if q == "64":
+            assert out["stats"]["walks_suspended"] > 0
+        assert pc["bitexact"] >= parity.MIN_BITEXACT, pc
+        assert out["stats"]["world_rays"] == int(ref["stats"][0])

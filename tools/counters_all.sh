@@ -21,4 +21,6 @@ s4 --scene s4 --spp 256
 s5 --scene s5 --spp 256
 s2_d100 --scene s2 --divs 100
 s4_real --scene s4_real --spp 256
+ball --scene ball
+random --scene random
 CFG
