@@ -2512,150 +2512,6 @@ SRR_D int coop_mixture(const SceneView& S, const DiffSetup& me, bool& pend, int&
   return rounds;
 }
 
-// ------------------------------------ wave-cooperative Beckmann mixture loop
-// The resampling loop of a Beckmann bounce (Raytracing_n.cpp:75-89 over pdf.h:119-156)
-// takes 1.3-1.4 attempts per path but the wave's slowest Beckmann lane 2.6-2.8 (C4,
-// C4_real), and every attempt of the BSDF branch is a full Beckmann sample (visible
-// normals by Newton-bisection, pbrt-v3's BeckmannSample11): the branch ran for its
-// slowest lane.  So only the first attempt runs per lane (beck_first); the paths
-// still pending then share all 64 lanes, helper k of a path taking attempt tries + k:
-// * its RNG states: the LCG (branch draw; light: index draw + 2) and the PCG stream
-//   (BSDF: two pcg_uniform) after k attempts, a function of the LCG state alone
-//   (skip_beck_attempt);
-// * its pdf needs the beckmann_pdf's value of the latest BSDF-branch attempt before
-//   it (value() returns what generate() last stored, 0 before the first),
-//   so each helper returns its light pdf and, for a BSDF attempt, the value it
-//   generated, and the path's owner folds its helpers in attempt order: the carried
-//   value, each attempt's 0.5 * light + 0.5 * carried (the reference's double
-//   arithmetic), the first non-zero one wins;
-// bit for bit the sequential loop's result, RNG states included.
-// A Beckmann bounce's setup lives in the diffuse bounce's DiffSetup registers (a lane
-// has one or the other): p the hit point, w / v the onb, nl the incoming ray direction
-// (world: beckmann_pdf::generate's wo), c0 / c1 the distribution's alpha x / y, flags
-// kBeckFlag.
-constexpr int kBeckFlag = 4;
-SRR_D DiffSetup beck_setup(const Bsdf& f, V3 p, V3 wo) {
-  return DiffSetup{p, f.uvw.w, f.uvw.v, wo, f.dist.ax, f.dist.ay, kBeckFlag};
-}
-SRR_D Bsdf beck_bsdf(const DiffSetup& d) {
-  Bsdf f;
-  f.kind = MAT_BECKMANN;
-  f.uvw.w = d.w;
-  f.uvw.v = d.v;
-  f.uvw.u = cross(d.w, d.v);
-  f.n = d.w;
-  f.dist.ax = d.c0;
-  f.dist.ay = d.c1;
-  f.beck_pdf = 0;
-  return f;
-}
-
-// one attempt's draws and results: the light pdf of its direction, and for a BSDF
-// attempt (is_b) the value generate() stored in f.beck_pdf
-SRR_D void beck_attempt(const SceneView& S, Bsdf& f, V3 wo, V3 hpt, Rng& rng, V3& nd, float& lp, bool& is_b) {
-  is_b = !(drand(rng) < 0.5);
-  if (!is_b) nd = lights_random(S, hpt, rng);
-  else nd = bsdf_generate<true>(f, wo, rng);
-  lp = lights_pdf(S, hpt, nd);
-}
-
-SRR_D uint64_t pcg_step(uint64_t p) { return p * 0x5851f42d4c957f2dULL + kPcgInc; }
-
-// the LCG and PCG states after one Beckmann attempt's draws, from the LCG state before it
-SRR_D void skip_beck_attempt(const SceneView& S, uint64_t& s, uint64_t& p) {
-  s = lcg_step(s);        // drand() < 0.5: the branch
-  if ((s >> 47) == 0) {   // light: hitable_list::random (hitable_list.h:63-67)
-    s = lcg_step(s);
-    const int idx = int((double)(uint32_t)(s >> 16) / 4294967296.0 * S.n_lights);
-    if (S.lights[idx].kind != LIGHT_NONE) s = lcg_step(lcg_step(s));
-  } else {
-    p = pcg_step(pcg_step(p));  // beckmann_pdf::generate: two UniformFloat (pdf.h:137-138)
-  }
-}
-
-// Runs to completion the loops of every lane with `pend` (converged wave, all 64 lanes
-// active): in, the lane's setup, RNG states before attempt `tries` and in `cp` the
-// carried beckmann_pdf value; out, ndir, in `cp` the pdf, and the RNG states after the
-// first attempt with pdf != 0 (or the guard's last attempt).
-SRR_D int coop_beck(const SceneView& S, const DiffSetup& me, bool& pend, int& tries, Rng& rng, V3& ndir, float& cp) {
-  int rounds = 0;
-  const int lane = lane_id();
-  const uint64_t lt = (1ull << lane) - 1;
-  uint64_t F = __ballot(pend);
-  while (F) {
-    const int nF = __popcll(F);
-    const int rank = pend ? __popcll(F & lt) : nF + __popcll(~F & lt);
-    const int owner_of = __builtin_amdgcn_ds_permute(rank << 2, lane);
-    const int q = lane % nF;
-    const int k = lane / nF;
-    const int src = __builtin_amdgcn_ds_bpermute(q << 2, owner_of);
-    DiffSetup d;
-    d.p = v3(__shfl(me.p.x, src), __shfl(me.p.y, src), __shfl(me.p.z, src));
-    d.w = v3(__shfl(me.w.x, src), __shfl(me.w.y, src), __shfl(me.w.z, src));
-    d.v = v3(__shfl(me.v.x, src), __shfl(me.v.y, src), __shfl(me.v.z, src));
-    d.nl = v3(__shfl(me.nl.x, src), __shfl(me.nl.y, src), __shfl(me.nl.z, src));
-    d.c0 = __shfl(me.c0, src);
-    d.c1 = __shfl(me.c1, src);
-    const int t0 = __shfl(tries, src);
-    uint64_t s = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(rng.lcg >> 32), src) << 32) |
-                 (uint32_t)__shfl((int)(uint32_t)rng.lcg, src);
-    uint64_t sp = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(rng.pcg >> 32), src) << 32) |
-                  (uint32_t)__shfl((int)(uint32_t)rng.pcg, src);
-    const bool active = t0 + k < kMixtureGuard;
-    V3 nd = v3(0.f);
-    float lp = 0, gen = 0;
-    bool is_b = false;
-    if (active) {
-      for (int j = 0; j < k; ++j) skip_beck_attempt(S, s, sp);
-      Rng rr{s, sp};
-      Bsdf f = beck_bsdf(d);
-      beck_attempt(S, f, d.nl, d.p, rr, nd, lp, is_b);
-      gen = f.beck_pdf;
-      s = rr.lcg;
-      sp = rr.pcg;
-    }
-    // the owner folds its helpers in attempt order: the first with a non-zero pdf
-    // (or the guard's last attempt) wins; else the path goes on after all of them
-    int m = 0, j = 0, last = lane;  // helpers; the one folded last
-    bool done = false;
-    float c = cp, wp = 0;
-    if (pend) m = min((63 - rank) / nF + 1, kMixtureGuard - tries);
-    while (__ballot(j < m && !done)) {
-      const int h = min(rank + j * nF, 63);
-      const bool hb = __shfl((int)is_b, h) != 0;
-      const float hg = __shfl(gen, h), hl = __shfl(lp, h);
-      if (j < m && !done) {
-        if (hb) c = hg;
-        const float pv = 0.5 * hl + 0.5 * c;  // (Raytracing_n.cpp:81: double arithmetic, one rounding)
-        last = h;
-        wp = pv;
-        done = pv != 0 || tries + j + 1 >= kMixtureGuard;  // (a NaN pdf ends the loop too)
-      }
-      ++j;
-    }
-    const float wx = __shfl(nd.x, last), wy = __shfl(nd.y, last), wz = __shfl(nd.z, last);
-    const uint64_t ws = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(s >> 32), last) << 32) |
-                        (uint32_t)__shfl((int)(uint32_t)s, last);
-    const uint64_t wsp = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(sp >> 32), last) << 32) |
-                         (uint32_t)__shfl((int)(uint32_t)sp, last);
-    if (pend) {  // the state after the attempt folded last: the winner's, or the round's last
-      rng.lcg = ws;
-      rng.pcg = wsp;
-      if (done) {
-        ndir = v3(wx, wy, wz);
-        cp = wp;
-        pend = false;
-      } else {
-        cp = c;
-        tries += m;
-      }
-    }
-    F = __ballot(pend);
-    ++rounds;
-  }
-  return rounds;
-}
-
 // camera::get_ray(s, t) (camera.h:51-59; random_in_unit_disk camera.h:8-14)
 SRR_D void camera_get_ray(const DCamera& C, float u, float v, Rng& rng, V3& o, V3& dir, float& time) {
   V3 pd;
@@ -2687,9 +2543,6 @@ SRR_D void camera_get_ray(const DCamera& C, float u, float v, Rng& rng, V3& o, V
 // tangent plane -- and evaluates exactly only light-branch attempts, near-tangent
 // BSDF samples, and the guard's last attempt.  The attempts it evaluates and
 // their results are the sequential loop's, bit for bit.
-#ifndef SRR_BCOOP
-#define SRR_BCOOP 1  // Beckmann resampling loops past their first attempt run wave-cooperatively (A/B: -DSRR_BCOOP=0)
-#endif
 #ifndef SRR_MIXTURE_SKIP
 #define SRR_MIXTURE_SKIP 2
 #endif
@@ -3483,7 +3336,7 @@ __global__ void __launch_bounds__(BS, MINB) SRR_PATHS_VGPR_ATTR k_paths(PathsArg
     V3 C = v3(0.f);
     // a diffuse bounce with lights: set up here, its mixture loop runs below with
     // the whole wave (coop_mixture), then its record is written
-    bool diff = false, pend = false, bpend = false;  // (bpend: a Beckmann loop, coop_beck)
+    bool diff = false, pend = false;
     int natt = 0;  // (TIMED: mixture attempts of this lane's Beckmann scatter)
     uint64_t fam_dt[3] = {0, 0, 0};  // (TIMED: this lane's ticks in the BECK / SPEC / DIFF-set-up branch)
     DiffSetup ds{};
@@ -3591,22 +3444,6 @@ __global__ void __launch_bounds__(BS, MINB) SRR_PATHS_VGPR_ATTR k_paths(PathsArg
         }
         if (fam == FAM_TERM) {
           C = hit_emitted(S, h.mat, r.d, h.p, h.n, h.u, h.v);
-        } else if (ALLFAM && SRR_BCOOP && fam == FAM_BECK && S.n_lights > 0) {
-          // scatter<FAM_BECK> up to its resampling loop, which the wave's Beckmann lanes
-          // then run together (coop_beck), and the record after it
-          const DMat M = S.mats[h.mat];
-          d_atten = tex_value(S, M.tex, h.u, h.v, h.p);
-          Bsdf f;
-          f.dist.ax = M.p[0];
-          f.dist.ay = M.p[1];
-          f.uvw = onb_from_w(h.n);
-          (void)drand(rng);  // mixture_pdf ctor (pdf.h:175)
-          ds = beck_setup(f, h.p, r.d);
-          d_pdf = 0;  // the carried beckmann_pdf value: none generated yet
-          d_n = h.n;
-          d_tries = 0;
-          diff = bpend = true;
-          done = false;
         } else if ((!ALLFAM || fam == FAM_DIFF) && S.n_lights > 0) {
           // scatter<FAM_DIFF> up to its resampling loop (Raytracing_n.cpp:73-75)
           const DMat M = S.mats[h.mat];
@@ -3683,24 +3520,12 @@ __global__ void __launch_bounds__(BS, MINB) SRR_PATHS_VGPR_ATTR k_paths(PathsArg
       }
       max_rounds = max(max_rounds, (uint32_t)rounds);
     }
-    if (ALLFAM && SRR_BCOOP && __ballot(bpend)) {
-      const SceneView S = view();
-      const uint64_t tc = TIMED ? __builtin_amdgcn_s_memtime() : 0;
-      const int rounds = coop_beck(S, ds, bpend, d_tries, rng, d_dir, d_pdf);
-      if (TIMED) tf[0] += __builtin_amdgcn_s_memtime() - tc;  // (the Beckmann branch's wave time)
-      max_rounds = max(max_rounds, (uint32_t)rounds);
-    }
-    if (diff) {  // the rest of scatter<FAM_DIFF> / <FAM_BECK>: scattering_pdf and the record
+    if (diff) {  // the rest of scatter<FAM_DIFF>: scattering_pdf and the record
       const PathWork W = work();
       if (d_pdf == 0) n_events += kCapped;  // the loop reached kMixtureGuard
-      V3 as;
-      if (ALLFAM && SRR_BCOOP && ds.flags == kBeckFlag) {
-        as = d_atten * scattering_pdf<true>(beck_bsdf(ds), d_n, r.d, d_dir);
-      } else {
-        float c = dot(d_n, unit_vector(d_dir));  // material.h:100-105, 134-138
-        if (c < 0) c = 0;
-        as = d_atten * (c / kPi);
-      }
+      float c = dot(d_n, unit_vector(d_dir));  // material.h:100-105, 134-138
+      if (c < 0) c = 0;
+      const V3 as = d_atten * (c / kPi);
       if (depth >= W.max_depth || slot >= W.lanes) atomicOr(W.err, 2);
       else rec_store(rec_at(W, depth), make_float4(as.x, as.y, as.z, d_pdf));
       r = Ray{ds.p, d_dir, r.tm};
