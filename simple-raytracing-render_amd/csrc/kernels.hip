@@ -1843,9 +1843,12 @@ SRR_D V3 tex_value_slow(const SceneView& S, int ti, float u, float v, V3 p) {
       if (i > T.nx - 1) i = T.nx - 1;
       if (j > T.ny - 1) j = T.ny - 1;
       const uint8_t* px = S.images + T.off + 3 * (size_t)i + 3 * (size_t)T.nx * j;
-      float r = int(px[0]) / 255.0;
-      float g = int(px[1]) / 255.0;
-      float b = int(px[2]) / 255.0;
+      // int(px[c]) / 255.0 is a double quotient rounded to float; for each of the 256
+      // byte values it equals the float quotient (float)x / 255.0f (tests/test_texture_quotient.py),
+      // which saves three double divisions per lookup
+      float r = (float)int(px[0]) / 255.0f;
+      float g = (float)int(px[1]) / 255.0f;
+      float b = (float)int(px[2]) / 255.0f;
       return v3(r, g, b);
     }
     if (T.kind == TEX_CHECKER) {
@@ -2004,17 +2007,24 @@ SRR_D void beckmann_sample11(float cosThetaI, float u1, float u2, float& sx, flo
   const float SQRT_PI_INV = (float)(1.f / ::sqrt(kPi));
   float normalization = 1 / (1 + c + SQRT_PI_INV * tanThetaI * rexp(-cotThetaI * cotThetaI));
   int it = 0;
+  // (a loop that stops on |value| < 1e-5 has just computed ErfInv of the final b:
+  // the reference's ErfInv(b) after the loop is that same value, so it is reused)
+  float invErf = 0;
+  bool fresh = false;
   while (++it < 10) {
     if (!(b >= a && b <= c)) b = 0.5f * (a + c);
-    float invErf = ErfInv(b);
+    invErf = ErfInv(b);
     float value = normalization * (1 + b + SQRT_PI_INV * tanThetaI * (rexp(-invErf * invErf))) - sample_x;
     float derivative = normalization * (1 - invErf * tanThetaI);
-    if (fabsf(value) < 1e-5f) break;
+    if (fabsf(value) < 1e-5f) {
+      fresh = true;
+      break;
+    }
     if (value > 0) c = b;
     else a = b;
     b -= value / derivative;
   }
-  sx = ErfInv(b);
+  sx = fresh ? invErf : ErfInv(b);
   sy = ErfInv(2.0f * fmaxf(u2, 1e-6f) - 1.0f);
 }
 
