@@ -3694,9 +3694,11 @@ __global__ void __launch_bounds__(256) k_accumulate_window(const float* sample, 
   acc_write(acc, o, 3 * (size_t)lp, cx, cy, cz);
 }
 
-// The same sums with 16-byte loads, for windows of a multiple of kAccChunk samples:
-// a pixel's chunk is 12 contiguous float4 (16-byte aligned), so a block fetches
-// its 256 x 16 samples with 12 float4 loads per thread (no per-element division).
+// The same sums with 16-byte loads, for windows of a multiple of 4 samples: a pixel's
+// row of 3 x spp_w floats is then 16-byte aligned and its chunk of 16 samples is 12
+// contiguous float4, so a block fetches its 256 x 16 samples with 12 float4 loads per
+// thread (no per-element division); a window's last 4, 8 or 12 samples (spp_w % 16:
+// the 1080p windows are 344 samples) go through the same tile as one shorter chunk.
 __global__ void __launch_bounds__(256) k_accumulate_window16(const float4* sample4, int npix, int spp_w, float* acc,
                                                              int init, AccOut o) {
   __shared__ float tile[256 * (3 * kAccChunk + 1)];
@@ -3704,6 +3706,7 @@ __global__ void __launch_bounds__(256) k_accumulate_window16(const float4* sampl
   const int p0 = blockIdx.x * 256;
   const int lp = p0 + threadIdx.x;
   const int np = min(256, npix - p0);
+  const int s_full = spp_w - spp_w % kAccChunk;  // samples in whole chunks
   float cx = 0, cy = 0, cz = 0;
   if (lp < npix && !init) {
     cx = acc[3 * (size_t)lp];
@@ -3722,8 +3725,8 @@ __global__ void __launch_bounds__(256) k_accumulate_window16(const float4* sampl
         v[j] = ntl(&base[((size_t)px * spp_w + s0) * 3 / 4 + f4]);
       }
     };
-    fetch(0);
-    for (int s0 = 0; s0 < spp_w; s0 += kAccChunk) {
+    if (s_full > 0) fetch(0);
+    for (int s0 = 0; s0 < s_full; s0 += kAccChunk) {
 #pragma unroll
       for (int j = 0; j < kQ; ++j) {
         const int i = threadIdx.x + 256 * j, px = i / kQ, f4 = i - px * kQ;
@@ -3734,7 +3737,7 @@ __global__ void __launch_bounds__(256) k_accumulate_window16(const float4* sampl
         d[3] = v[j].w;
       }
       __syncthreads();
-      if (s0 + kAccChunk < spp_w) fetch(s0 + kAccChunk);
+      if (s0 + kAccChunk < s_full) fetch(s0 + kAccChunk);
       const float* t = &tile[threadIdx.x * (3 * kAccChunk + 1)];
 #pragma unroll
       for (int k = 0; k < kAccChunk; ++k) {
@@ -3744,13 +3747,35 @@ __global__ void __launch_bounds__(256) k_accumulate_window16(const float4* sampl
       }
       __syncthreads();
     }
-    acc_write(acc, o, 3 * (size_t)lp, cx, cy, cz);
-    return;
+  } else {
+    for (int s0 = 0; s0 < s_full; s0 += kAccChunk) {
+      for (int i = threadIdx.x; i < np * kQ; i += 256) {
+        const int px = i / kQ, f4 = i - px * kQ;
+        const float4 v = ntl(&sample4[((size_t)(p0 + px) * spp_w + s0) * 3 / 4 + f4]);
+        float* d = &tile[px * (3 * kAccChunk + 1) + 4 * f4];
+        d[0] = v.x;
+        d[1] = v.y;
+        d[2] = v.z;
+        d[3] = v.w;
+      }
+      __syncthreads();
+      if (lp < npix) {
+        const float* t = &tile[threadIdx.x * (3 * kAccChunk + 1)];
+#pragma unroll
+        for (int k = 0; k < kAccChunk; ++k) {
+          cx += t[3 * k];
+          cy += t[3 * k + 1];
+          cz += t[3 * k + 2];
+        }
+      }
+      __syncthreads();
+    }
   }
-  for (int s0 = 0; s0 < spp_w; s0 += kAccChunk) {
-    for (int i = threadIdx.x; i < np * kQ; i += 256) {
-      const int px = i / kQ, f4 = i - px * kQ;
-      const float4 v = ntl(&sample4[((size_t)(p0 + px) * spp_w + s0) * 3 / 4 + f4]);
+  if (s_full < spp_w) {  // the last n = 4, 8 or 12 samples: 3n / 4 float4 per pixel
+    const int n = spp_w - s_full, qn = 3 * n / 4;
+    for (int i = threadIdx.x; i < np * qn; i += 256) {
+      const int px = i / qn, f4 = i - px * qn;
+      const float4 v = ntl(&sample4[((size_t)(p0 + px) * spp_w + s_full) * 3 / 4 + f4]);
       float* d = &tile[px * (3 * kAccChunk + 1) + 4 * f4];
       d[0] = v.x;
       d[1] = v.y;
@@ -3760,14 +3785,12 @@ __global__ void __launch_bounds__(256) k_accumulate_window16(const float4* sampl
     __syncthreads();
     if (lp < npix) {
       const float* t = &tile[threadIdx.x * (3 * kAccChunk + 1)];
-#pragma unroll
-      for (int k = 0; k < kAccChunk; ++k) {
+      for (int k = 0; k < n; ++k) {
         cx += t[3 * k];
         cy += t[3 * k + 1];
         cz += t[3 * k + 2];
       }
     }
-    __syncthreads();
   }
   if (lp >= npix) return;
   acc_write(acc, o, 3 * (size_t)lp, cx, cy, cz);
@@ -4304,7 +4327,7 @@ void launch_accumulate_window(const float* sample, int npix, int spp_w, float* a
                               float* out, int scale_ns) {
   static const bool scalar = getenv("SRR_ACC_SCALAR") != nullptr;  // A/B diagnostics
   const dev::AccOut o{out, scale_ns};
-  if (spp_w % dev::kAccChunk == 0 && ((uintptr_t)sample & 15) == 0 && !scalar)
+  if (spp_w % 4 == 0 && ((uintptr_t)sample & 15) == 0 && !scalar)
     hipLaunchKernelGGL(dev::k_accumulate_window16, dim3((npix + 255) / 256), dim3(256), 0, st, (const float4*)sample,
                        npix, spp_w, acc, init ? 1 : 0, o);
   else

@@ -434,8 +434,11 @@ static int paths_enqueue(srr_renderer* r, FrameSlot& F, const srr_params* p, boo
   budget /= (size_t)std::max(1, r->window_share);
   // (k_paths numbers a window's paths in 32 bits: npix * W < 2^31)
   const int64_t w_max = std::max<int64_t>(1, (((int64_t)1 << 31) - 1) / std::max<int64_t>(1, npix));
-  const int W = (int)std::max<int64_t>(
+  int W = (int)std::max<int64_t>(
       1, std::min<int64_t>(std::min<int64_t>(p->spp, w_max), (int64_t)(budget / (12 * (size_t)npix))));
+  // a window of a multiple of 4 samples is summed with 16-byte loads (k_accumulate_window16;
+  // 1080p: 345 -> 344 samples, still 3 windows of 1,024); the sums do not depend on W
+  if (W < p->spp && W >= 16) W &= ~3;
   if ((int64_t)npix * W >= ((int64_t)1 << 31)) {
     err = "frame too large for one sample window (npix >= 2^31)";
     return SRR_EINVAL;

@@ -130,6 +130,31 @@ def test_sample_windows_do_not_change_the_frame(monkeypatch):
     np.testing.assert_array_equal(many["rays"], one["rays"])
 
 
+@pytest.mark.parametrize("nx,ny,spp,window_mb,launches", [
+    # 16 MiB / (12 B x 65,536 px) = 21 -> windows of 20, 20, 20, 4: 16-sample chunks, then a
+    # 4-sample tail chunk; the last window is a tail chunk alone
+    (256, 256, 64, "16", 4),
+    # 32,500 px (the last block holds 244): 37 -> windows of 36 (two chunks + a tail of 4) and 4
+    (250, 130, 40, "14", 2),
+    # 29 -> 28: a chunk and a tail of 12; the last window (8) a tail chunk alone
+    (256, 256, 64, "22", 3),
+    # 58 -> 56: three chunks and a tail of 8; the last window (38) takes the scalar kernel
+    (128, 128, 150, "11", 3),
+])
+def test_windows_of_a_multiple_of_four_samples(monkeypatch, nx, ny, spp, window_mb, launches):
+    """Path engine: windows of >= 16 samples are cut to a multiple of 4 and summed with
+    16-byte loads (k_accumulate_window16), including a last chunk of 4, 8 or 12 samples;
+    the frame is the one-window frame bit for bit (the running sums keep sample order)."""
+    sc, _ = scenes.s2_cornell_teapot()
+    r = capi.Renderer(sc.text())
+    one = r.render(nx, ny, spp, 50)
+    monkeypatch.setenv("SRR_WINDOW_MB", window_mb)
+    many = r.render(nx, ny, spp, 50)
+    assert one["stats"]["trace_launches"] == 1
+    assert many["stats"]["trace_launches"] == launches, many["stats"]
+    np.testing.assert_array_equal(many["mean"].view(np.uint32), one["mean"].view(np.uint32))
+
+
 @pytest.mark.parametrize("factory,nx,ny,spp", [
     (scenes.s2_cornell_teapot, 256, 256, 16),
     (lambda: scenes.s3_cornell_teapot_microfacet("beckmann"), 256, 256, 16),
