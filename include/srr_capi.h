@@ -237,7 +237,7 @@ int srr_render_device(srr_renderer* r, const srr_params* p, float* d_mean, srr_s
  * of another frame in flight, before srr_render_wait(ticket) returns; enqueueing
  * a third frame first finishes the oldest (its stats stay for its wait).
  * Device memory: each frame in flight holds its own sample window (all shard
- * pixels x the window's samples x 12 B, at most SRR_WINDOW_MB, default 8 GiB),
+ * pixels x the window's samples x 12 B, at most SRR_WINDOW_MB, default 16 GiB),
  * bounce records (16 B x max_depth per persistent lane) and sums; the
  * synchronous slot keeps its own window too, so alternating the two modes
  * reallocates nothing (the other mode's windows are given back only when an

@@ -428,8 +428,10 @@ static int paths_enqueue(srr_renderer* r, FrameSlot& F, const srr_params* p, boo
   // without the feature (read per frame: tests switch it between renders)
   const char* wq_env = getenv("SRR_WALK_Q");
   const int walk_q = wq_env ? std::max(0, std::min(64, atoi(wq_env))) : r->walk_q_default;
-  // sample window: all pixels x W samples, buffer within SRR_WINDOW_MB (default 8192)
-  size_t budget = (size_t)8192 << 20;
+  // sample window: all pixels x W samples, buffer within SRR_WINDOW_MB (default 16384: a
+  // 1080p frame of 1,024 spp in 2 windows, not 3 -- one drain and one serial accumulation
+  // fewer)
+  size_t budget = (size_t)16384 << 20;
   if (const char* e = getenv("SRR_WINDOW_MB")) budget = (size_t)std::max(1, atoi(e)) << 20;
   budget /= (size_t)std::max(1, r->window_share);
   // (k_paths numbers a window's paths in 32 bits: npix * W < 2^31)

@@ -48,6 +48,15 @@ def lib():
     if _LIB is None:
         if not os.path.exists(LIB_PATH):
             raise SrrError(f"{LIB_PATH} not built (run __graft_entry__.build() or make -C simple-raytracing-render_amd)")
+        # One HIP runtime per process: torch ships its own libamdhip64.so.7 (the same SONAME
+        # as /opt/rocm's, which libsrr.so's RUNPATH names), and whichever is loaded first
+        # serves both.  Loaded first, /opt/rocm's left torch unable to initialise the GPU
+        # afterwards ("No HIP GPUs are available", tools/torch_after_render.py), so when
+        # torch is installed its runtime is loaded before libsrr.so.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         vp, ip, cp = ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p
         L.srr_last_error.restype = cp

@@ -115,7 +115,7 @@ def test_c3_full_frame_is_the_reference_frame(name):
 def test_1080p_sample_windows_are_the_reference_frame(name, monkeypatch):
     """A 1080p frame cut into sample windows (renderer.cpp paths_enqueue: a window
     holds as many samples of every pixel as SRR_WINDOW_MB allows; the bench's C4
-    frame runs 3 per frame): SRR_WINDOW_MB=150 gives windows of 6, 6 and 4 of the
+    frame runs 2 per frame): SRR_WINDOW_MB=150 gives windows of 6, 6 and 4 of the
     16 samples, so each pixel's paths come from three k_paths launches and are summed
     across two window boundaries -- every path and every pixel group still the
     reference's."""
