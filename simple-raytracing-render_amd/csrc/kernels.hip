@@ -2044,6 +2044,94 @@ SRR_D V3 beckmann_sample_wh(const Beck& d, V3 wo, float u1, float u2) {  // :12-
   return wh;
 }
 
+// The terms of one Beckmann sample that depend only on the incoming direction: computed
+// once per scatter by bsdf_prepare<true>, where the reference recomputes them on every
+// attempt of the resampling loop (pdf.h:136-152 -> :12-32, :34-107).  Same expressions,
+// so the same values; the per-attempt part below takes them from here.
+struct BeckPre {
+  V3 wwo;            // the local unit -wo (pdf.h:140)
+  V3 uw;             // unit_vector(wwo) (Reflect's)
+  float cphi, sphi;  // CosPhi / SinPhi of the stretched direction ws
+  float ct;          // ws.z: BeckmannSample11's cosThetaI
+  float tan_t, c, fit, norm;  // its tanThetaI, Erf(cosThetaI), fit, normalization (ct <= .9999)
+  float lam1;        // 1 + Lambda(wo): G(wo, wi)'s first two terms
+  bool flip;         // wwo.z < 0
+};
+
+SRR_D void beckmann_pre(const Beck& d, const Onb& uvw, V3 wo, BeckPre& p) {
+  const V3 mwo = -wo;
+  p.wwo = unit_vector(v3(dot(mwo, uvw.u), dot(mwo, uvw.v), dot(mwo, uvw.w)));
+  p.uw = unit_vector(p.wwo);
+  p.flip = p.wwo.z < 0;
+  const V3 wi = p.flip ? -p.wwo : p.wwo;
+  const V3 ws = unit_vector(v3(d.ax * wi.x, d.ay * wi.y, wi.z));
+  p.cphi = CosPhi(ws);
+  p.sphi = SinPhi(ws);
+  p.ct = ws.z;
+  p.tan_t = p.c = p.fit = p.norm = 0;
+  if (!(p.ct > .9999)) {
+    const float cosThetaI = p.ct;
+    float sinThetaI = rsqrt_exact(fmaxf(0.0f, 1.0f - cosThetaI * cosThetaI));
+    float tanThetaI = sinThetaI / cosThetaI;
+    float cotThetaI = 1 / tanThetaI;
+    p.c = Erf(cosThetaI);
+    float thetaI = racos(cosThetaI);
+    p.fit = 1 + thetaI * (-0.876f + thetaI * (0.4265f - 0.0594f * thetaI));
+    const float SQRT_PI_INV = (float)(1.f / ::sqrt(kPi));
+    p.norm = 1 / (1 + p.c + SQRT_PI_INV * tanThetaI * rexp(-cotThetaI * cotThetaI));
+    p.tan_t = tanThetaI;
+  }
+  p.lam1 = 1 + d.Lambda(wo);
+}
+
+// beckmann_sample11 with its direction terms from BeckPre
+SRR_D void beckmann_sample11_pre(const BeckPre& p, float u1, float u2, float& sx, float& sy) {
+  if (p.ct > .9999) {
+    float r = rsqrt_exact(-rlog(1.0f - u1));
+    float sinPhi = ::sin(2 * kPi * u2);
+    float cosPhi = ::cos(2 * kPi * u2);
+    sx = r * cosPhi;
+    sy = r * sinPhi;
+    return;
+  }
+  const float tanThetaI = p.tan_t, normalization = p.norm;
+  float a = -1, c = p.c;
+  float sample_x = fmaxf(u1, 1e-6f);
+  float b = c - (1 + c) * rpow(1 - sample_x, p.fit);
+  const float SQRT_PI_INV = (float)(1.f / ::sqrt(kPi));
+  int it = 0;
+  float invErf = 0;
+  bool fresh = false;
+  while (++it < 10) {
+    if (!(b >= a && b <= c)) b = 0.5f * (a + c);
+    invErf = ErfInv(b);
+    float value = normalization * (1 + b + SQRT_PI_INV * tanThetaI * (rexp(-invErf * invErf))) - sample_x;
+    float derivative = normalization * (1 - invErf * tanThetaI);
+    if (fabsf(value) < 1e-5f) {
+      fresh = true;
+      break;
+    }
+    if (value > 0) c = b;
+    else a = b;
+    b -= value / derivative;
+  }
+  sx = fresh ? invErf : ErfInv(b);
+  sy = ErfInv(2.0f * fmaxf(u2, 1e-6f) - 1.0f);
+}
+
+SRR_D V3 beckmann_sample_wh_pre(const Beck& d, const BeckPre& p, float u1, float u2) {
+  float sx, sy;
+  beckmann_sample11_pre(p, u1, u2, sx, sy);
+  float tmp = p.cphi * sx - p.sphi * sy;
+  sy = p.sphi * sx + p.cphi * sy;
+  sx = tmp;
+  sx = d.ax * sx;
+  sy = d.ay * sy;
+  V3 wh = unit_vector(v3(-sx, -sy, 1.f));
+  if (p.flip) wh = -wh;
+  return wh;
+}
+
 #ifndef SRR_SINCOS
 #define SRR_SINCOS 1  // random_cosine_direction's sine and cosine from one sincosf_ (A/B: -DSRR_SINCOS=0)
 #endif
@@ -2221,6 +2309,7 @@ struct Bsdf {
   float co;        // cosine_pdf: dot(unit_vector(wo), n)
   V3 lo;           // onrennayar_pdf: local unit(-wo)
   bool flip;       // cosine_pdf / onrennayar_pdf generate: dot(-wo, n) > 0
+  BeckPre bp;      // beckmann: the sample's incoming-direction terms (bsdf_prepare<true>)
 };
 
 SRR_D V3 to_local_unit(const Onb& b, V3 d) {
@@ -2231,16 +2320,16 @@ SRR_D V3 to_local_unit(const Onb& b, V3 d) {
 template <bool BECK>
 SRR_D V3 bsdf_generate(Bsdf& f, V3 wo, Rng& rng) {
   if (BECK) {  // pdf.h:136-152
+    (void)wo;  // (its terms are in f.bp, from bsdf_prepare<true>)
     float u1 = pcg_uniform(rng);
     float u2 = pcg_uniform(rng);
-    V3 mwo = -wo;
-    V3 wwo = unit_vector(v3(dot(mwo, f.uvw.u), dot(mwo, f.uvw.v), dot(mwo, f.uvw.w)));
-    V3 wh = beckmann_sample_wh(f.dist, wwo, u1, u2);
-    V3 uw = unit_vector(wwo);
-    V3 wi = -uw + 2 * dot(uw, wh) * wh;  // Reflect (reflection.h:34-36)
+    const BeckPre& p = f.bp;
+    V3 wh = beckmann_sample_wh_pre(f.dist, p, u1, u2);
+    V3 wi = -p.uw + 2 * dot(p.uw, wh) * wh;  // Reflect (reflection.h:34-36)
     V3 wwi = unit_vector(wi.x * f.uvw.u + wi.y * f.uvw.v + wi.z * f.uvw.w);
-    f.beck_pdf = f.dist.D(wh) * f.dist.G(wo, wi) / (4 * AbsCosTheta(wi) * AbsCosTheta(wwo));
-    if (!(wi.z * wwo.z > 0)) f.beck_pdf = 0;
+    // D(wh) * G(wo, wi), G = 1 / (1 + Lambda(wo) + Lambda(wi))
+    f.beck_pdf = f.dist.D(wh) * (1 / (p.lam1 + f.dist.Lambda(wi))) / (4 * AbsCosTheta(wi) * AbsCosTheta(p.wwo));
+    if (!(wi.z * p.wwo.z > 0)) f.beck_pdf = 0;
     return wwi;
   }
   // cosine_pdf / onrennayar_pdf (pdf.h:47-56, 103-112)
@@ -2251,7 +2340,10 @@ SRR_D V3 bsdf_generate(Bsdf& f, V3 wo, Rng& rng) {
 
 template <bool BECK>
 SRR_D void bsdf_prepare(Bsdf& f, V3 wo) {
-  if (BECK) return;
+  if (BECK) {
+    beckmann_pre(f.dist, f.uvw, wo, f.bp);
+    return;
+  }
   f.flip = dot(-wo, f.n) > 0;
   // (both fields written on every path: one of them left unset kept f in scratch)
   float co = 0;
@@ -3939,6 +4031,7 @@ __global__ void k_kat(int kind, int n, int w, float* rec, const float* aux, cons
       f.beck_pdf = 0;
       const V3 wo = kat3(r + 5);
       Rng rng{0, kat_pcg(r + 8)};
+      bsdf_prepare<true>(f, wo);
       const V3 wi = bsdf_generate<true>(f, wo, rng);
       kat_put3(r + 12, wi);
       r[15] = bsdf_value<true>(f, wo, wi);
